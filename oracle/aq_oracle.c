@@ -1,0 +1,307 @@
+/*
+ * oracle/aq_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity oracle).
+ *
+ * This file is the CPU restatement of the reference's hot path. Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as
+ * the checker or the timed CPU baseline. The product (ppls_amd/, include/) never links it.
+ *
+ * What it restates (all citations into /root/reference/aquadPartA.c):
+ *   - the integrand macro  F(arg) cosh(arg)*cosh(arg)*cosh(arg)*cosh(arg)      :46
+ *   - the worker task body (trapezoid on [l,r] and both halves, strict '>')   :183-202
+ *   - the farmer's accumulation result += area and LIFO bag order            :149, :152-159
+ *   - task counting (one task per interval dispatched)                       :162
+ * and, because the hot path's transcendental lives in a third-party dependency that is
+ * NOT under /root/reference, glibc 2.35 libm (Ubuntu 2.35-0ubuntu3.11):
+ *   - __ieee754_cosh   (sysdeps/ieee754/dbl-64/e_cosh.c, fdlibm formula)
+ *   - __exp            (sysdeps/ieee754/dbl-64/e_exp.c, N=128 table; FMA and non-FMA ifunc forms)
+ *   - __expm1          (sysdeps/ieee754/dbl-64/s_expm1.c, k=0 path, Estrin polynomial)
+ * Pinning: tests/test_oracle.py checks these bit for bit against the host libm and the
+ * whole tree walk against the reference's header known answer (aquadPartA.c:31-36) and
+ * against fixtures produced by the compiled reference (oracle/Makefile -> oracle/_ref/).
+ *
+ * Build: oracle/Makefile -> oracle/_build/liboracle.so (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <quadmath.h>
+
+#include "glibc_exp_table.h"
+
+#define AQO_OK 0
+#define AQO_EINVAL (-1)
+#define AQO_EDEPTH (-5)
+#define AQO_ENOMEM (-6)
+
+/* integrand ids: same numbering as include/aquad.h */
+#define AQO_F_COSH4 0     /* aquadPartA.c:46 */
+#define AQO_F_SIN_RECIP 1 /* sin(1/x): the SURVEY config-4 variant of the F macro */
+
+static inline uint64_t asu(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
+static inline double asd(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
+
+/* ---- glibc 2.35 exp, e_exp.c main path (valid for |x| in [2^-54, 709.78]) -------------- */
+static const double InvLn2N = 0x1.71547652b82fep7;
+static const double Shift = 0x1.8p52;
+static const double NegLn2hiN = -0x1.62e42fefa0000p-8;
+static const double NegLn2loN = -0x1.cf79abc9e3b3ap-47;
+static const double C2 = 0x1.ffffffffffdbdp-2;
+static const double C3 = 0x1.555555555543cp-3;
+static const double C4 = 0x1.55555cf172b91p-5;
+static const double C5 = 0x1.1111167a4d017p-7;
+
+/* FMA ifunc form (__exp_fma): GCC contracts z+Shift, r, tmp and scale+scale*tmp. */
+double aqo_exp_fma(double x)
+{
+    uint32_t abstop = (uint32_t)(asu(x) >> 52) & 0x7ff;
+    int large = abstop >= 0x408; /* |x| >= 512: glibc's specialcase() */
+    if (abstop >= 0x409 && x > 0x1.62e42fefa39efp+9) return INFINITY;
+    double kd = fma(InvLn2N, x, Shift);
+    uint64_t ki = asu(kd);
+    kd -= Shift;
+    double r = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x));
+    uint64_t idx = 2 * (ki % 128);
+    uint64_t top = ki << 45;
+    double tail = asd(aqo_exp_tab[idx]);
+    uint64_t sbits = aqo_exp_tab[idx + 1] + top;
+    double r2 = r * r;
+    double tmp = fma(r2 * r2, fma(r, C5, C4), fma(r2, fma(r, C3, C2), tail + r));
+    if (large) { /* specialcase, k > 0 branch */
+        sbits -= 1009ull << 52;
+        double scale = asd(sbits);
+        return 0x1p1009 * fma(scale, tmp, scale);
+    }
+    double scale = asd(sbits);
+    return fma(scale, tmp, scale);
+}
+
+/* Non-FMA ifunc form (__exp_sse2): same source, no contraction (this file: -ffp-contract=off). */
+double aqo_exp_nofma(double x)
+{
+    uint32_t abstop = (uint32_t)(asu(x) >> 52) & 0x7ff;
+    int large = abstop >= 0x408;
+    if (abstop >= 0x409 && x > 0x1.62e42fefa39efp+9) return INFINITY;
+    double z = InvLn2N * x;
+    double kd = z + Shift;
+    uint64_t ki = asu(kd);
+    kd -= Shift;
+    double r = x + kd * NegLn2hiN + kd * NegLn2loN;
+    uint64_t idx = 2 * (ki % 128);
+    uint64_t top = ki << 45;
+    double tail = asd(aqo_exp_tab[idx]);
+    uint64_t sbits = aqo_exp_tab[idx + 1] + top;
+    double r2 = r * r;
+    double tmp = tail + r + r2 * (C2 + r * C3) + r2 * r2 * (C4 + r * C5);
+    if (large) {
+        sbits -= 1009ull << 52;
+        double scale = asd(sbits);
+        return 0x1p1009 * (scale + scale * tmp);
+    }
+    double scale = asd(sbits);
+    return scale + scale * tmp;
+}
+
+/* ---- glibc 2.35 expm1, s_expm1.c, the |x| < 0.5*ln2 (k = 0) path ----------------------- */
+static const double Q1 = -3.33333333333331316428e-02;
+static const double Q2 = 1.58730158725481460165e-03;
+static const double Q3 = -7.93650757867487942473e-05;
+static const double Q4 = 4.00821782732936239552e-06;
+static const double Q5 = -2.01099218183624371326e-07;
+
+double aqo_expm1_small(double x)
+{
+    uint32_t hx = (uint32_t)(asu(x) >> 32) & 0x7fffffff;
+    if (hx < 0x3c900000) return x; /* |x| < 2^-54 */
+    double hfx = 0.5 * x;
+    double hxs = x * hfx;
+    double R1 = 1.0 + hxs * Q1;
+    double h2 = hxs * hxs;
+    double R2 = Q2 + hxs * Q3;
+    double h4 = h2 * h2;
+    double R3 = Q4 + hxs * Q5;
+    double r1 = R1 + h2 * R2 + h4 * R3;
+    double t = 3.0 - r1 * hfx;
+    double e = hxs * ((r1 - t) / (6.0 - x * t));
+    return x - (x * e - hxs);
+}
+
+/* ---- glibc 2.35 __ieee754_cosh (e_cosh.c) ----------------------------------------------- */
+double aqo_cosh(double x, int fma_variant)
+{
+    uint32_t ix = (uint32_t)(asu(x) >> 32) & 0x7fffffff;
+    double ax = fabs(x);
+    if (ix < 0x40360000) { /* |x| < 22 */
+        if (ix < 0x3fd62e43) { /* |x| < 0.5*ln2 */
+            if (ix < 0x3c800000) return 1.0;
+            double t = aqo_expm1_small(ax);
+            double w = 1.0 + t;
+            return 1.0 + (t * t) / (w + w);
+        }
+        double t = fma_variant ? aqo_exp_fma(ax) : aqo_exp_nofma(ax);
+        return 0.5 * t + 0.5 / t;
+    }
+    if (ix >= 0x7ff00000) return x * x; /* inf / nan */
+    if (ix < 0x40862e42) return 0.5 * (fma_variant ? aqo_exp_fma(ax) : aqo_exp_nofma(ax));
+    /* |x| in [log(maxdouble), overflowthreshold] */
+    if (ax <= 0x1.633ce8fb9f87dp+9) {
+        double w = fma_variant ? aqo_exp_fma(0.5 * ax) : aqo_exp_nofma(0.5 * ax);
+        double t = 0.5 * w;
+        return t * w;
+    }
+    return INFINITY;
+}
+
+/* libm modes for F: restated glibc (FMA / non-FMA ifunc forms) or the host libm itself. */
+#define AQO_LIBM_RESTATED_FMA 0
+#define AQO_LIBM_RESTATED_NOFMA 1
+#define AQO_LIBM_HOST 2
+
+/* F(arg) exactly as the reference macro expands: cosh(a)*cosh(a)*cosh(a)*cosh(a), left to right. */
+static inline double F_eval(int integrand, int mode, double x)
+{
+    if (integrand == AQO_F_SIN_RECIP) return sin(1.0 / x);
+    double c;
+    if (mode == AQO_LIBM_HOST) c = cosh(x);
+    else c = aqo_cosh(x, mode == AQO_LIBM_RESTATED_FMA);
+    return c * c * c * c;
+}
+
+double aqo_F(int integrand, int mode, double x) { return F_eval(integrand, mode, x); }
+
+void aqo_cosh_array(int mode, long n, const double *x, double *out)
+{
+    for (long i = 0; i < n; i++) {
+        if (mode == AQO_LIBM_HOST) out[i] = cosh(x[i]);
+        else out[i] = aqo_cosh(x[i], mode == AQO_LIBM_RESTATED_FMA);
+    }
+}
+
+void aqo_exp_array(int mode, long n, const double *x, double *out)
+{
+    for (long i = 0; i < n; i++) {
+        if (mode == AQO_LIBM_HOST) out[i] = exp(x[i]);
+        else out[i] = mode == AQO_LIBM_RESTATED_FMA ? aqo_exp_fma(x[i]) : aqo_exp_nofma(x[i]);
+    }
+}
+
+void aqo_expm1_array(int mode, long n, const double *x, double *out)
+{
+    for (long i = 0; i < n; i++) out[i] = mode == AQO_LIBM_HOST ? expm1(x[i]) : aqo_expm1_small(x[i]);
+}
+
+/* ---- the tree walk --------------------------------------------------------------------- */
+typedef struct {
+    double area_lifo;     /* Σ leaf areas in the reference's P=2 arrival order (LIFO, :149) */
+    double area_quad_hi;  /* exact-ish Σ leaf areas accumulated in __float128, hi part      */
+    double area_quad_lo;  /*                                                   lo part      */
+    uint64_t tasks;       /* intervals evaluated (= Σ tasks_per_process, :162)              */
+    uint64_t leaves;      /* accepted intervals (messages with tag 1 carrying an area, :201) */
+    int32_t levels;       /* 1 + deepest depth reached                                       */
+    int32_t pad;
+} aqo_result;
+
+typedef struct { double l, r, fl, fr; int32_t depth; } rec_t;
+
+/*
+ * Depth-first walk in exactly the reference's LIFO bag order (aquadPartA.c:152-159: children
+ * pushed [l,mid] then [mid,r], so [mid,r] pops first). With one worker (mpirun -n 2) the
+ * reference's arrival order is this order, so area_lifo is its printed area bit for bit.
+ * Records carry (fl, fr): the child's lrarea (:185) is token-for-token the parent's larea /
+ * rarea expression (:189-190) with the same operands, so this is bit-exact with recomputing.
+ * tasks_per_level / leaves_per_level: caller arrays of length maxlev (may be NULL).
+ */
+int aqo_integrate(int integrand, int mode, double a, double b, double eps, int maxlev,
+                  aqo_result *res, uint64_t *tasks_per_level, uint64_t *leaves_per_level)
+{
+    if (!res || maxlev <= 0 || maxlev > 4096 || !(b >= a)) return AQO_EINVAL;
+    memset(res, 0, sizeof(*res));
+    if (tasks_per_level) memset(tasks_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    if (leaves_per_level) memset(leaves_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    size_t cap = 256, n = 0;
+    rec_t *st = (rec_t *)malloc(cap * sizeof(rec_t));
+    if (!st) return AQO_ENOMEM;
+    st[n++] = (rec_t){a, b, F_eval(integrand, mode, a), F_eval(integrand, mode, b), 0};
+    double area = 0.0;
+    __float128 q = 0;
+    int rc = AQO_OK;
+    while (n) {
+        rec_t t = st[--n];
+        if (t.depth >= maxlev) { rc = AQO_EDEPTH; break; }
+        double left = t.l, right = t.r;
+        double lrarea = (t.fl + t.fr) * (right - left) / 2;          /* :185 */
+        double mid = (left + right) / 2;                              /* :187 */
+        double fmid = F_eval(integrand, mode, mid);                   /* :188 */
+        double larea = (t.fl + fmid) * (mid - left) / 2;              /* :189 */
+        double rarea = (fmid + t.fr) * (right - mid) / 2;             /* :190 */
+        res->tasks++;
+        if (tasks_per_level) tasks_per_level[t.depth]++;
+        if (t.depth + 1 > res->levels) res->levels = t.depth + 1;
+        if (fabs((larea + rarea) - lrarea) > eps) {                   /* :191 */
+            if (n + 2 > cap) {
+                cap *= 2;
+                rec_t *ns = (rec_t *)realloc(st, cap * sizeof(rec_t));
+                if (!ns) { rc = AQO_ENOMEM; break; }
+                st = ns;
+            }
+            st[n++] = (rec_t){left, mid, t.fl, fmid, t.depth + 1};    /* :192-194 push [l,mid] */
+            st[n++] = (rec_t){mid, right, fmid, t.fr, t.depth + 1};   /* :195-197 push [mid,r] */
+        } else {
+            double acc = larea + rarea;                               /* :199 */
+            area += acc;                                              /* :149 */
+            q += (__float128)acc;
+            res->leaves++;
+            if (leaves_per_level) leaves_per_level[t.depth]++;
+        }
+    }
+    free(st);
+    res->area_lifo = area;
+    res->area_quad_hi = (double)q;
+    res->area_quad_lo = (double)(q - (__float128)res->area_quad_hi);
+    return rc;
+}
+
+/* Quad sum as a decimal string (for fixtures). */
+int aqo_quad_to_string(double hi, double lo, char *buf, int len)
+{
+    __float128 q = (__float128)hi + (__float128)lo;
+    return quadmath_snprintf(buf, (size_t)len, "%.25Qg", q);
+}
+
+/* ---- batch: splitmix64 bounds ------------------------------------ */
+static inline uint64_t splitmix64_next(uint64_t *state)
+{
+    uint64_t z = (*state += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+/* Generate n bounds pairs: a = 5*u1, b = 5*u2, swapped if a > b (state0 = 0x9E3779B97F4A7C15). */
+void aqo_batch_bounds(long n, double *a, double *b)
+{
+    uint64_t s = 0x9E3779B97F4A7C15ULL;
+    for (long i = 0; i < n; i++) {
+        double u1 = (double)(splitmix64_next(&s) >> 11) * 0x1.0p-53;
+        double u2 = (double)(splitmix64_next(&s) >> 11) * 0x1.0p-53;
+        double x = 5.0 * u1, y = 5.0 * u2;
+        if (x > y) { double t = x; x = y; y = t; }
+        a[i] = x;
+        b[i] = y;
+    }
+}
+
+/* Integrate each [a[i], b[i]] independently; per-integral area (quad-accumulated) and counts. */
+int aqo_integrate_batch(int integrand, int mode, long n, const double *a, const double *b,
+                        double eps, int maxlev, double *area, uint64_t *tasks, uint64_t *leaves)
+{
+    for (long i = 0; i < n; i++) {
+        aqo_result r;
+        int rc = aqo_integrate(integrand, mode, a[i], b[i], eps, maxlev, &r, NULL, NULL);
+        if (rc) return rc;
+        if (area) area[i] = r.area_quad_hi + r.area_quad_lo;
+        if (tasks) tasks[i] = r.tasks;
+        if (leaves) leaves[i] = r.leaves;
+    }
+    return AQO_OK;
+}
