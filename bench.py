@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: accepted subintervals/s (+ FP64 F-evals/s) for the reference integrand at EPSILON=1e-10.
+
+Workload (BASELINE.json configs[1]): F(x)=cosh(x)^4 (aquadPartA.c:46) over [0,5] (:47-48) at
+EPSILON=1e-10 -- 1 464 273 tasks, 732 137 accepted subintervals per integral. One step = one
+complete integral through the hot path (persistent on-device farmer, ppls_amd/csrc/aquad.hip).
+With N ranks (one process per GPU, torch.distributed backend "nccl" = RCCL) every step is sharded:
+rank r evaluates shard r of N of the SAME integral (strong scaling); the partial results of the
+K timed steps are combined with ONE all-reduce inside the timed region. Steps are pipelined
+(aq_integrate_async, no host sync between integrals); every step's counts are verified
+bit-exactly against the golden tree after timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--eps E] [--no-cpu-baseline]
+
+Prints ONE JSON line (rank 0). `value` = accepted subintervals/s over all GPUs; roofline is the
+persistent kernel's FP64 rate (38 algorithmic FLOP per task) over its HIP-event
+launch time, against the 78.6 TFLOP/s FP64 vector peak of one MI355X; cpu_baseline is the
+reference binary (oracle/_ref, compiled from /root/reference) run under mpirun on this host's
+cores, or the oracle restatement when that binary cannot run.
+"""
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FLOP_PER_TASK = 38          # exp 20 + cosh tail 3 + pow4 3 + step 12
+FP64_PEAK = 78.6e12         # MI355X FP64 vector peak (256 CU x 2.4 GHz x 128 FLOP/clk), MI355X_MICROARCH.md
+GOLDEN = {1e-10: (1464273, 732137), 1e-12: (6606491, 3303246), 1e-8: (319295, 159648), 1e-3: (6567, 3284)}
+
+
+def cpu_baseline(eps, target_s=12.0):
+    """Time the reference on this host's CPU cores (bounded sample), before any GPU init."""
+    tag = {1e-3: "1e-3", 1e-10: "1e-10", 1e-12: "1e-12"}.get(eps, "none")
+    ref = os.path.join(ROOT, "oracle", "_ref", "aquadPartA_eps" + tag)
+    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    nprocs = max(2, min(8, ncpu))  # farmer + up to 7 workers (the survey's P=8 config)
+    tasks_golden, leaves_golden = GOLDEN.get(eps, (None, None))
+    if os.path.exists(ref) and os.path.exists(mpirun) and leaves_golden:
+        try:
+            runs, t_total = 0, 0.0
+            while t_total < target_s and runs < 50:
+                t0 = time.perf_counter()
+                out = subprocess.run([mpirun, "-n", str(nprocs), ref], capture_output=True, text=True, timeout=120,
+                                     check=True).stdout
+                t_total += time.perf_counter() - t0
+                runs += 1
+                counts = [int(v) for v in out.strip().splitlines()[-1].split()]
+                if sum(counts) != tasks_golden:
+                    raise RuntimeError("reference task total mismatch")
+            return {"value": leaves_golden * runs / t_total, "unit": "accepted subintervals/s", "cores": nprocs,
+                    "kind": "reference",
+                    "sample": f"{runs} full runs of the reference binary (eps={eps}) under mpirun -n {nprocs} "
+                              f"(farmer + {nprocs - 1} workers), {t_total:.1f} s wall incl. MPI startup"}
+        except Exception as e:  # fall back to the restatement
+            print(f"cpu_baseline: reference binary unusable ({e}); timing the oracle port", file=sys.stderr)
+    from oracle import pyoracle as O
+    runs, t_total, leaves = 0, 0.0, 0
+    while t_total < target_s and runs < 400:
+        t0 = time.perf_counter()
+        r = O.integrate(eps=eps)
+        t_total += time.perf_counter() - t0
+        runs += 1
+        leaves += r.leaves
+    return {"value": leaves / t_total, "unit": "accepted subintervals/s", "cores": 1, "kind": "port",
+            "sample": f"{runs} full integrals by the oracle's sequential restatement (1 thread), {t_total:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per launch of the persistent kernel from the committed PMC profile (or None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--eps", type=float, default=1e-10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    # CPU baseline first: before this process touches the GPU (child processes only).
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.eps)
+
+    import torch
+    import torch.distributed as dist
+    from ppls_amd import Context, Problem
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    ctx = Context(local_rank)
+    ctx.set_level_histograms(False)
+    problem = Problem(eps=args.eps)
+    nslots = ctx.async_slots
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def run_steps(k, first_slot=0):
+        for i in range(k):
+            ctx.integrate_async(problem, (first_slot + i) % nslots, rank, world)
+
+    # warmup (also validates)
+    run_steps(args.warmup)
+    ctx.synchronize()
+
+    K = args.steps
+    buf = torch.zeros((min(K, nslots), 4), dtype=torch.float64, device="cuda")
+    totals = torch.zeros((K, 4), dtype=torch.float64, device="cuda")
+    ctx.kernel_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    while done < K:
+        m = min(K - done, nslots)
+        run_steps(m, 0)
+        ctx.gather_results(0, m, buf.data_ptr())
+        ctx.synchronize()
+        chunk = buf[:m]
+        if world > 1:
+            dist.all_reduce(chunk, op=dist.ReduceOp.SUM)
+        totals[done:done + m] = chunk
+        done += m
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    kern_ms, launches = ctx.kernel_time()
+    ctx.kernel_timing(False)
+
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_avg_ms = float(tt[0]), float(tt[1])
+    else:
+        kern_avg_ms = kern_ms / max(launches, 1)
+
+    # verify every timed step against the golden tree
+    tot = totals.cpu().numpy()
+    tg, lg = GOLDEN.get(args.eps, (None, None))
+    ok = bool((tot[:, 3] == 0).all())
+    if tg is not None:
+        ok = ok and bool((tot[:, 1] == tg).all() and (tot[:, 2] == lg).all())
+    accepted_total = float(tot[:, 2].sum())
+    tasks_total = float(tot[:, 1].sum())
+    f_evals = tasks_total + 2 * K   # algorithmic F evaluations: 1 per task + F(A), F(B) per integral
+
+    # this rank's share of the tasks per launch, for the roofline of its kernel
+    mine = ctx.fetch((K - 1) % nslots)
+    achieved = FLOP_PER_TASK * mine.tasks / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
+
+    if rank == 0:
+        out = {
+            "metric": "accepted subintervals/sec + FP64 F-evals/sec at 1/2/4/8 MI355X, EPSILON=1e-10",
+            "value": accepted_total / elapsed,
+            "unit": "accepted subintervals/s",
+            "f_evals_per_sec": f_evals / elapsed,
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (analytic integrand, no dataset)",
+            "config": {"workload": "cosh4 on [0,5], EPSILON=%g, one integral per step (BASELINE configs[1])" % args.eps,
+                       "integrand": "cosh(x)^4 (aquadPartA.c:46)", "a": 0.0, "b": 5.0, "eps": args.eps,
+                       "tasks_per_integral": int(tot[0, 1]), "accepted_per_integral": int(tot[0, 2]),
+                       "parallelism": f"shard{world}" if world > 1 else "single-gpu",
+                       "workgroups_per_gpu": ctx.num_cus},
+            "verified": ok,
+            "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(),
+                         "kernel": "aq::k_persist<0,false>", "kernel_avg_us": kern_avg_ms * 1e3,
+                         "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": mine.tasks},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

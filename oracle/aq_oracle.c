@@ -203,31 +203,43 @@ typedef struct {
 
 typedef struct { double l, r, fl, fr; int32_t depth; } rec_t;
 
-/*
- * Depth-first walk in exactly the reference's LIFO bag order (aquadPartA.c:152-159: children
- * pushed [l,mid] then [mid,r], so [mid,r] pops first). With one worker (mpirun -n 2) the
- * reference's arrival order is this order, so area_lifo is its printed area bit for bit.
- * Records carry (fl, fr): the child's lrarea (:185) is token-for-token the parent's larea /
- * rarea expression (:189-190) with the same operands, so this is bit-exact with recomputing.
- * tasks_per_level / leaves_per_level: caller arrays of length maxlev (may be NULL).
- */
-int aqo_integrate(int integrand, int mode, double a, double b, double eps, int maxlev,
-                  aqo_result *res, uint64_t *tasks_per_level, uint64_t *leaves_per_level)
+typedef struct {
+    double area;
+    __float128 q;
+    int rc;
+} acc_t;
+
+static int push_rec(rec_t **st, size_t *n, size_t *cap, rec_t r)
 {
-    if (!res || maxlev <= 0 || maxlev > 4096 || !(b >= a)) return AQO_EINVAL;
-    memset(res, 0, sizeof(*res));
-    if (tasks_per_level) memset(tasks_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
-    if (leaves_per_level) memset(leaves_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    if (*n + 1 > *cap) {
+        size_t nc = *cap * 2;
+        rec_t *ns = (rec_t *)realloc(*st, nc * sizeof(rec_t));
+        if (!ns) return AQO_ENOMEM;
+        *st = ns;
+        *cap = nc;
+    }
+    (*st)[(*n)++] = r;
+    return AQO_OK;
+}
+
+/*
+ * Depth-first walk of the subtree rooted at `root`, in exactly the reference's LIFO bag order
+ * (aquadPartA.c:152-159: children pushed [l,mid] then [mid,r], so [mid,r] pops first). With one
+ * worker (mpirun -n 2) the reference's arrival order is this order, so acc->area is its printed
+ * area bit for bit. Records carry (fl, fr): the child's lrarea (:185) is token-for-token the
+ * parent's larea / rarea expression (:189-190) with the same operands, so this is bit-exact with
+ * the reference's recomputation.
+ */
+static void walk(int integrand, int mode, rec_t root, double eps, int maxlev, aqo_result *res, acc_t *acc,
+                 uint64_t *tpl, uint64_t *lpl)
+{
     size_t cap = 256, n = 0;
     rec_t *st = (rec_t *)malloc(cap * sizeof(rec_t));
-    if (!st) return AQO_ENOMEM;
-    st[n++] = (rec_t){a, b, F_eval(integrand, mode, a), F_eval(integrand, mode, b), 0};
-    double area = 0.0;
-    __float128 q = 0;
-    int rc = AQO_OK;
+    if (!st) { acc->rc = AQO_ENOMEM; return; }
+    st[n++] = root;
     while (n) {
         rec_t t = st[--n];
-        if (t.depth >= maxlev) { rc = AQO_EDEPTH; break; }
+        if (t.depth >= maxlev) { acc->rc = AQO_EDEPTH; break; }
         double left = t.l, right = t.r;
         double lrarea = (t.fl + t.fr) * (right - left) / 2;          /* :185 */
         double mid = (left + right) / 2;                              /* :187 */
@@ -235,30 +247,119 @@ int aqo_integrate(int integrand, int mode, double a, double b, double eps, int m
         double larea = (t.fl + fmid) * (mid - left) / 2;              /* :189 */
         double rarea = (fmid + t.fr) * (right - mid) / 2;             /* :190 */
         res->tasks++;
-        if (tasks_per_level) tasks_per_level[t.depth]++;
+        if (tpl) tpl[t.depth]++;
         if (t.depth + 1 > res->levels) res->levels = t.depth + 1;
         if (fabs((larea + rarea) - lrarea) > eps) {                   /* :191 */
-            if (n + 2 > cap) {
-                cap *= 2;
-                rec_t *ns = (rec_t *)realloc(st, cap * sizeof(rec_t));
-                if (!ns) { rc = AQO_ENOMEM; break; }
-                st = ns;
+            if (push_rec(&st, &n, &cap, (rec_t){left, mid, t.fl, fmid, t.depth + 1}) ||   /* :192-194 */
+                push_rec(&st, &n, &cap, (rec_t){mid, right, fmid, t.fr, t.depth + 1})) {  /* :195-197 */
+                acc->rc = AQO_ENOMEM;
+                break;
             }
-            st[n++] = (rec_t){left, mid, t.fl, fmid, t.depth + 1};    /* :192-194 push [l,mid] */
-            st[n++] = (rec_t){mid, right, fmid, t.fr, t.depth + 1};   /* :195-197 push [mid,r] */
         } else {
-            double acc = larea + rarea;                               /* :199 */
-            area += acc;                                              /* :149 */
-            q += (__float128)acc;
+            double v = larea + rarea;                                 /* :199 */
+            acc->area += v;                                           /* :149 */
+            acc->q += (__float128)v;
             res->leaves++;
-            if (leaves_per_level) leaves_per_level[t.depth]++;
+            if (lpl) lpl[t.depth]++;
         }
     }
     free(st);
-    res->area_lifo = area;
-    res->area_quad_hi = (double)q;
-    res->area_quad_lo = (double)(q - (__float128)res->area_quad_hi);
-    return rc;
+}
+
+static void finish(aqo_result *res, const acc_t *acc)
+{
+    res->area_lifo = acc->area;
+    res->area_quad_hi = (double)acc->q;
+    res->area_quad_lo = (double)(acc->q - (__float128)res->area_quad_hi);
+}
+
+/* The whole tree from the root [a,b]. tasks_per_level / leaves_per_level: length maxlev or NULL. */
+int aqo_integrate(int integrand, int mode, double a, double b, double eps, int maxlev,
+                  aqo_result *res, uint64_t *tasks_per_level, uint64_t *leaves_per_level)
+{
+    if (!res || maxlev <= 0 || maxlev > 4096 || !(b >= a)) return AQO_EINVAL;
+    memset(res, 0, sizeof(*res));
+    if (tasks_per_level) memset(tasks_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    if (leaves_per_level) memset(leaves_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    acc_t acc = {0.0, 0, AQO_OK};
+    rec_t root = {a, b, F_eval(integrand, mode, a), F_eval(integrand, mode, b), 0};
+    walk(integrand, mode, root, eps, maxlev, res, &acc, tasks_per_level, leaves_per_level);
+    finish(res, &acc);
+    return acc.rc;
+}
+
+/*
+ * The share of shard `shard` of `nshards` in the device's partition (ppls_amd/csrc/aquad.hip,
+ * k_persist seeding): V = G*nshards virtual workers, seed depth D = ceil(log2 V) + S; virtual
+ * worker vwg = w*nshards + shard owns the depth-D positions j = k*V + (k odd ? V-1-vwg : vwg) < 2^D;
+ * a task above depth D is counted by the owner of its leftmost descendant position. Summing the
+ * results of all shards gives aqo_integrate()'s counts exactly (tests check both properties).
+ */
+int aqo_integrate_shard(int integrand, int mode, double a, double b, double eps, int maxlev, int G, int S,
+                        int shard, int nshards, aqo_result *res, uint64_t *tasks_per_level,
+                        uint64_t *leaves_per_level)
+{
+    if (!res || maxlev <= 0 || maxlev > 4096 || !(b >= a) || G < 1 || S < 0 || S > 6 || nshards < 1 ||
+        shard < 0 || shard >= nshards)
+        return AQO_EINVAL;
+    memset(res, 0, sizeof(*res));
+    if (tasks_per_level) memset(tasks_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    if (leaves_per_level) memset(leaves_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
+    const uint64_t V = (uint64_t)G * (uint64_t)nshards;
+    int D = 0;
+    while ((1ull << D) < V) D++;
+    D += S;
+    const uint64_t npos = 1ull << D;
+    const uint64_t nbands = (npos + V - 1) / V;
+    const double fa = F_eval(integrand, mode, a), fb = F_eval(integrand, mode, b);
+    acc_t acc = {0.0, 0, AQO_OK};
+    for (int w = 0; w < G && acc.rc == AQO_OK; w++) {
+        const uint64_t vwg = (uint64_t)w * (uint64_t)nshards + (uint64_t)shard;
+        for (uint64_t k = 0; k < nbands && acc.rc == AQO_OK; k++) {
+            const uint64_t p = k * V + ((k & 1) ? (V - 1 - vwg) : vwg);
+            if (p >= npos) continue;
+            double l = a, r = b, fl = fa, fr = fb;
+            int alive = 1;
+            for (int d = 0; d < D; d++) {
+                const double mid = (l + r) / 2;
+                const double fmid = F_eval(integrand, mode, mid);
+                const double lrarea = (fl + fr) * (r - l) / 2;
+                const double larea = (fl + fmid) * (mid - l) / 2;
+                const double rarea = (fmid + fr) * (r - mid) / 2;
+                const int refine = fabs((larea + rarea) - lrarea) > eps;
+                const int owner = (p & ((1ull << (D - d)) - 1ull)) == 0ull;
+                if (owner) {
+                    res->tasks++;
+                    if (tasks_per_level) tasks_per_level[d]++;
+                    if (d + 1 > res->levels) res->levels = d + 1;
+                }
+                if (!refine) {
+                    if (owner) {
+                        double v = larea + rarea;
+                        acc.area += v;
+                        acc.q += (__float128)v;
+                        res->leaves++;
+                        if (leaves_per_level) leaves_per_level[d]++;
+                    }
+                    alive = 0;
+                    break;
+                }
+                if (d + 1 >= maxlev) {
+                    if (owner) acc.rc = AQO_EDEPTH;
+                    alive = 0;
+                    break;
+                }
+                if ((p >> (D - 1 - d)) & 1ull) { l = mid; fl = fmid; }
+                else { r = mid; fr = fmid; }
+            }
+            if (alive) {
+                rec_t root = {l, r, fl, fr, D};
+                walk(integrand, mode, root, eps, maxlev, res, &acc, tasks_per_level, leaves_per_level);
+            }
+        }
+    }
+    finish(res, &acc);
+    return acc.rc;
 }
 
 /* Quad sum as a decimal string (for fixtures). */

@@ -73,6 +73,10 @@ def lib():
         for name in ("aqo_cosh_array", "aqo_exp_array", "aqo_expm1_array"):
             getattr(L, name).argtypes = [ctypes.c_int, ctypes.c_long, dp, dp]
             getattr(L, name).restype = None
+        L.aqo_integrate_shard.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(_Res), up, up]
+        L.aqo_integrate_shard.restype = ctypes.c_int
         L.aqo_F.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.aqo_F.restype = ctypes.c_double
         L.aqo_quad_to_string.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_char_p, ctypes.c_int]
@@ -101,6 +105,24 @@ def integrate(integrand=COSH4, a=0.0, b=5.0, eps=1e-3, mode=RESTATED_FMA, maxlev
     rc = L.aqo_integrate(integrand, mode, a, b, eps, maxlev, ctypes.byref(r), _up(tpl), _up(lpl))
     if rc != 0:
         raise RuntimeError(f"oracle aqo_integrate failed rc={rc}")
+    buf = ctypes.create_string_buffer(64)
+    L.aqo_quad_to_string(r.area_quad_hi, r.area_quad_lo, buf, 64)
+    n = r.levels
+    return OracleResult(r.area_lifo, r.area_quad_hi, r.area_quad_lo, buf.value.decode(), r.tasks, r.leaves,
+                        r.levels, [int(v) for v in tpl[:n]], [int(v) for v in lpl[:n]])
+
+
+def integrate_shard(shard, nshards, G=256, S=5, integrand=COSH4, a=0.0, b=5.0, eps=1e-3, mode=RESTATED_FMA,
+                    maxlev=256) -> OracleResult:
+    """Shard `shard` of `nshards` in the device's partition (G workgroups per GPU, 2^S seeds each)."""
+    L = lib()
+    r = _Res()
+    tpl = np.zeros(maxlev, np.uint64)
+    lpl = np.zeros(maxlev, np.uint64)
+    rc = L.aqo_integrate_shard(integrand, mode, a, b, eps, maxlev, G, S, shard, nshards, ctypes.byref(r), _up(tpl),
+                               _up(lpl))
+    if rc != 0:
+        raise RuntimeError(f"oracle aqo_integrate_shard failed rc={rc}")
     buf = ctypes.create_string_buffer(64)
     L.aqo_quad_to_string(r.area_quad_hi, r.area_quad_lo, buf, 64)
     n = r.levels

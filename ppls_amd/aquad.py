@@ -1,0 +1,244 @@
+"""Host-side mirror of the reference's interface for the quadrature path.
+
+Reference: /root/reference/aquadPartA.c
+  - EPSILON / F / A / B macros (:45-48)          -> Problem
+  - double farmer(int numprocs) (:125-173)         -> farmer(numprocs, problem) -> (area, tasks_per_process)
+  - the numprocs < 2 error (:86-90)                -> AquadError with the same message
+  - main()'s printout (:107-117)                   -> format_reference()
+Everything here calls the HIP engine through the C ABI (include/aquad.h). There is no CPU path.
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import _lib
+
+COSH4 = 0
+SIN_RECIP = 1
+INTEGRANDS = {"cosh4": COSH4, "sin_recip": SIN_RECIP}
+
+# aquadPartA.c:45-48
+DEFAULT_EPSILON = 1e-3
+DEFAULT_A = 0.0
+DEFAULT_B = 5.0
+
+ERR_NUMPROCS = "ERROR: Must have at least 2 processes to run"  # aquadPartA.c:87
+
+
+class AquadError(RuntimeError):
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
+
+
+@dataclass
+class Problem:
+    integrand: int = COSH4
+    a: float = DEFAULT_A
+    b: float = DEFAULT_B
+    eps: float = DEFAULT_EPSILON
+    max_depth: int = 0
+
+    def c(self):
+        f = self.integrand if isinstance(self.integrand, int) else INTEGRANDS[self.integrand]
+        return _lib.aq_problem(f, int(self.max_depth), float(self.a), float(self.b), float(self.eps))
+
+
+@dataclass
+class Result:
+    area: float
+    tasks: int
+    accepted: int
+    levels: int
+    n_cu: int
+    spilled: int = 0
+    tasks_per_cu: Dict[int, int] = field(default_factory=dict)
+    tasks_per_level: List[int] = field(default_factory=list)
+    leaves_per_level: List[int] = field(default_factory=list)
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = _lib.load().aq_strerror(rc).decode()
+        raise AquadError(f"{what}: {msg} (code {rc})", rc)
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _up(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _lib.load().aq_device_count(ctypes.byref(n))
+    return n.value
+
+
+class Context:
+    """One GPU: owns device memory, the stream and the on-device work queue (aq_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.L = _lib.load()
+        self._h = ctypes.c_void_p()
+        _check(self.L.aq_ctx_create(int(device), ctypes.byref(self._h)), "aq_ctx_create")
+        self.device = device
+        self.num_cus = self.L.aq_ctx_num_cus(self._h)
+
+    def close(self):
+        if self._h:
+            self.L.aq_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_level_histograms(self, enable: bool):
+        _check(self.L.aq_set_level_histograms(self._h, 1 if enable else 0), "aq_set_level_histograms")
+
+    # -- results ---------------------------------------------------------------------------
+    def _result(self, r, with_detail=True) -> Result:
+        out = Result(r.area, int(r.tasks), int(r.accepted), int(r.levels), int(r.n_cu), int(r.spilled))
+        if with_detail:
+            cu = np.zeros(_lib.AQ_CU_SLOTS, np.uint64)
+            self.L.aq_tasks_per_cu(self._h, _up(cu), _lib.AQ_CU_SLOTS)
+            out.tasks_per_cu = {int(i): int(cu[i]) for i in np.nonzero(cu)[0]}
+            t = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+            lv = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+            self.L.aq_level_histogram(self._h, _up(t), _up(lv), _lib.AQ_MAX_LEVELS)
+            n = out.levels
+            out.tasks_per_level = [int(v) for v in t[:n]]
+            out.leaves_per_level = [int(v) for v in lv[:n]]
+        return out
+
+    # -- the hot path ----------------------------------------------------------------------
+    def integrate(self, problem: Problem) -> Result:
+        r = _lib.aq_result()
+        _check(self.L.aq_integrate(self._h, ctypes.byref(problem.c()), ctypes.byref(r)), "aq_integrate")
+        return self._result(r)
+
+    def integrate_shard(self, problem: Problem, shard: int, nshards: int) -> Result:
+        r = _lib.aq_result()
+        _check(self.L.aq_integrate_shard(self._h, ctypes.byref(problem.c()), shard, nshards, ctypes.byref(r)),
+               "aq_integrate_shard")
+        return self._result(r)
+
+    def integrate_levels(self, problem: Problem) -> Result:
+        r = _lib.aq_result()
+        t = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+        lv = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+        _check(self.L.aq_integrate_levels(self._h, ctypes.byref(problem.c()), ctypes.byref(r), _up(t), _up(lv),
+                                          _lib.AQ_MAX_LEVELS), "aq_integrate_levels")
+        return self._result(r)
+
+    # -- async (bench) -----------------------------------------------------------------------
+    @property
+    def async_slots(self) -> int:
+        return self.L.aq_async_slots()
+
+    def integrate_async(self, problem: Problem, slot: int, shard: int = 0, nshards: int = 1):
+        _check(self.L.aq_integrate_async(self._h, ctypes.byref(problem.c()), shard, nshards, slot),
+               "aq_integrate_async")
+
+    def fetch(self, slot: int, detail=False) -> Result:
+        r = _lib.aq_result()
+        _check(self.L.aq_fetch(self._h, slot, ctypes.byref(r)), "aq_fetch")
+        return self._result(r, with_detail=detail)
+
+    def gather_results(self, first_slot: int, n: int, device_ptr: int):
+        """Enqueue slots' {area, tasks, accepted, error} rows into a device buffer (e.g. a torch tensor)."""
+        _check(self.L.aq_gather_results(self._h, first_slot, n, ctypes.c_void_p(device_ptr)), "aq_gather_results")
+
+    def synchronize(self):
+        _check(self.L.aq_synchronize(self._h), "aq_synchronize")
+
+    def kernel_timing(self, enable: bool):
+        _check(self.L.aq_kernel_timing(self._h, 1 if enable else 0), "aq_kernel_timing")
+
+    def kernel_time(self):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_uint64(0)
+        _check(self.L.aq_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), "aq_kernel_time")
+        return ms.value, n.value
+
+    # -- batch / libm ------------------------------------------------------------------------
+    def integrate_batch(self, a, b, eps, integrand=COSH4):
+        a = np.ascontiguousarray(a, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        n = a.size
+        area = np.empty(n, np.float64)
+        tasks = np.empty(n, np.uint64)
+        acc = np.empty(n, np.uint64)
+        _check(self.L.aq_integrate_batch(self._h, integrand, n, _dp(a), _dp(b), float(eps), _dp(area), _up(tasks),
+                                         _up(acc)), "aq_integrate_batch")
+        return area, tasks, acc
+
+    def eval_cosh(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        out = np.empty_like(x)
+        _check(self.L.aq_eval_cosh(self._h, x.size, _dp(x), _dp(out)), "aq_eval_cosh")
+        return out
+
+    def eval_integrand(self, x, integrand=COSH4):
+        x = np.ascontiguousarray(x, np.float64)
+        out = np.empty_like(x)
+        _check(self.L.aq_eval_integrand(self._h, integrand, x.size, _dp(x), _dp(out)), "aq_eval_integrand")
+        return out
+
+
+def integrate(integrand="cosh4", a=DEFAULT_A, b=DEFAULT_B, eps=DEFAULT_EPSILON, device=0, ctx=None) -> Result:
+    p = Problem(INTEGRANDS[integrand] if isinstance(integrand, str) else integrand, a, b, eps)
+    if ctx is not None:
+        return ctx.integrate(p)
+    with Context(device) as c:
+        return c.integrate(p)
+
+
+def group_tasks(tasks_per_cu: Dict[int, int], workers: int) -> List[int]:
+    """Map per-CU counters onto `workers` worker slots (CU k -> worker k mod workers, CUs in slot order)."""
+    out = [0] * workers
+    for k, slot in enumerate(sorted(tasks_per_cu)):
+        out[k % workers] += tasks_per_cu[slot]
+    return out
+
+
+def farmer(numprocs: int, problem: Optional[Problem] = None, ctx: Optional[Context] = None):
+    """Mirror of `double farmer(int numprocs)` + main()'s guard (aquadPartA.c:86-90, :125-173).
+
+    Returns (area, tasks_per_process) where tasks_per_process[0] is the farmer's 0 and entries
+    1..numprocs-1 are the on-device workers' task counts (the GPU's CUs grouped into numprocs-1 workers).
+    """
+    if numprocs < 2:
+        raise AquadError(ERR_NUMPROCS)
+    problem = problem or Problem()
+    own = ctx is None
+    ctx = ctx or Context(0)
+    try:
+        r = ctx.integrate(problem)
+    finally:
+        if own:
+            ctx.close()
+    return r.area, [0] + group_tasks(r.tasks_per_cu, numprocs - 1)
+
+
+def format_reference(area: float, tasks_per_process: List[int]) -> str:
+    """Exactly main()'s stdout (aquadPartA.c:107-117)."""
+    n = len(tasks_per_process)
+    s = "Area=%f\n" % area
+    s += "\nTasks Per Process\n"
+    s += "".join("%d\t" % i for i in range(n)) + "\n"
+    s += "".join("%d\t" % t for t in tasks_per_process) + "\n"
+    return s

@@ -1,0 +1,60 @@
+"""Build the MI355X extension in-tree: ppls_amd/_build/libaquad.so (+ the `aquad` CLI).
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the build container as well as on
+the GPU box. Flags that matter for parity:
+  -ffp-contract=off  the reference was compiled for baseline x86-64 (no FMA contraction); every
+                     fusion the device libm needs is an explicit __fma_rn() (aq_libm.h).
+  no -ffast-math     IEEE-correct f64 division (v_div_scale / v_div_fmas / v_div_fixup).
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT, "libaquad.so")
+CLI = os.path.join(OUT, "aquad")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+ARCH = os.environ.get("PPLS_AMD_ARCH", "gfx950")
+
+HIP_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+             "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+
+SOURCES = [os.path.join(CSRC, "aquad.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h")] + \
+    [os.path.join(ROOT, "include", "aquad.h")]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OUT, exist_ok=True)
+    tab = os.path.join(CSRC, "aq_exp_table.h")
+    if not os.path.exists(tab):
+        subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_exp_table.py")])
+    if force or _stale(LIB, DEPS):
+        cmd = [HIPCC] + HIP_FLAGS + ["-o", LIB] + SOURCES
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+    cli_src = os.path.join(CSRC, "aquad_cli.c")
+    if os.path.exists(cli_src) and (force or _stale(CLI, [cli_src, LIB])):
+        cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-I", os.path.join(ROOT, "include"), "-o", CLI, cli_src,
+               "-L", OUT, "-laquad", "-Wl,-rpath,$ORIGIN", "-lm"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print("built", LIB)

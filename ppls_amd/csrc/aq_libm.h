@@ -1,0 +1,129 @@
+// aq_libm.h -- device integrands for gfx950, bit-identical to the host the reference runs on.
+//
+// The reference's integrand is the macro F(arg) cosh(arg)*cosh(arg)*cosh(arg)*cosh(arg)
+// (/root/reference/aquadPartA.c:46), evaluated through glibc 2.35 libm. The accepted-interval
+// count at EPSILON=1e-10/1e-12 changes under a 1-ulp change of cosh, so the device
+// restates glibc's cosh exactly rather than calling OCML:
+//   __ieee754_cosh (e_cosh.c, fdlibm formula) over
+//   __exp          (e_exp.c, N=128 table, the FMA ifunc form x86_64 hosts with FMA select) and
+//   __expm1        (s_expm1.c, k = 0 path, Estrin polynomial, no fusion).
+// The kernels that include this header are compiled with -ffp-contract=off: every fusion below
+// is an explicit __fma_rn() placed exactly where GCC fused glibc's source.
+//
+// The 2 KiB exp table lives in LDS (one ds_read_b128 per lookup); kernels stage it at entry
+// with aq_stage_exp_table().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace aq {
+
+struct ExpEntry {  // tab[2k], tab[2k+1] of glibc's __exp_data.tab
+    uint64_t tail_bits;
+    uint64_t sbits;
+};
+
+static constexpr double kInvLn2N = 0x1.71547652b82fep7;
+static constexpr double kShift = 0x1.8p52;
+static constexpr double kNegLn2hiN = -0x1.62e42fefa0000p-8;
+static constexpr double kNegLn2loN = -0x1.cf79abc9e3b3ap-47;
+static constexpr double kC2 = 0x1.ffffffffffdbdp-2;
+static constexpr double kC3 = 0x1.555555555543cp-3;
+static constexpr double kC4 = 0x1.55555cf172b91p-5;
+static constexpr double kC5 = 0x1.1111167a4d017p-7;
+
+static constexpr double kQ1 = -3.33333333333331316428e-02;
+static constexpr double kQ2 = 1.58730158725481460165e-03;
+static constexpr double kQ3 = -7.93650757867487942473e-05;
+static constexpr double kQ4 = 4.00821782732936239552e-06;
+static constexpr double kQ5 = -2.01099218183624371326e-07;
+
+__device__ __forceinline__ uint32_t hi_word(double x) {
+    return (uint32_t)((uint64_t)__double_as_longlong(x) >> 32);
+}
+
+// glibc __exp_fma main path for x in [2^-54, 709.78]; x >= 512 takes glibc's specialcase scaling.
+__device__ __forceinline__ double exp_glibc(double x, const ExpEntry* __restrict__ tab) {
+    double kd = __fma_rn(kInvLn2N, x, kShift);
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd = kd - kShift;
+    const double r = __fma_rn(kd, kNegLn2loN, __fma_rn(kd, kNegLn2hiN, x));
+    const ExpEntry e = tab[ki & 127];
+    const double tail = __longlong_as_double((long long)e.tail_bits);
+    uint64_t sbits = e.sbits + (ki << 45);
+    const double r2 = r * r;
+    const double tmp = __fma_rn(r2 * r2, __fma_rn(r, kC5, kC4), __fma_rn(r2, __fma_rn(r, kC3, kC2), tail + r));
+    if (__builtin_expect(x >= 512.0, 0)) {
+        if (x > 0x1.62e42fefa39efp+9) return __longlong_as_double(0x7ff0000000000000LL);
+        sbits -= 1009ull << 52;
+        const double scale = __longlong_as_double((long long)sbits);
+        return 0x1p1009 * __fma_rn(scale, tmp, scale);
+    }
+    const double scale = __longlong_as_double((long long)sbits);
+    return __fma_rn(scale, tmp, scale);
+}
+
+// glibc __expm1 for |x| < 0.5*ln2 (the only range cosh passes it).
+__device__ __forceinline__ double expm1_glibc_small(double x) {
+    if ((hi_word(x) & 0x7fffffffu) < 0x3c900000u) return x;
+    const double hfx = 0.5 * x;
+    const double hxs = x * hfx;
+    const double R1 = 1.0 + hxs * kQ1;
+    const double h2 = hxs * hxs;
+    const double R2 = kQ2 + hxs * kQ3;
+    const double h4 = h2 * h2;
+    const double R3 = kQ4 + hxs * kQ5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    const double t = 3.0 - r1 * hfx;
+    const double e = hxs * ((r1 - t) / (6.0 - x * t));
+    return x - (x * e - hxs);
+}
+
+// glibc __ieee754_cosh.
+__device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restrict__ tab) {
+    const uint32_t ix = hi_word(x) & 0x7fffffffu;
+    const double ax = fabs(x);
+    if (__builtin_expect(ix < 0x40360000u, 1)) {          // |x| < 22
+        if (ix < 0x3fd62e43u) {                             // |x| < 0.5*ln2
+            if (ix < 0x3c800000u) return 1.0;
+            const double t = expm1_glibc_small(ax);
+            const double w = 1.0 + t;
+            return 1.0 + (t * t) / (w + w);
+        }
+        const double t = exp_glibc(ax, tab);
+        return 0.5 * t + 0.5 / t;
+    }
+    if (ix >= 0x7ff00000u) return x * x;
+    if (ix < 0x40862e42u) return 0.5 * exp_glibc(ax, tab);
+    if (ax <= 0x1.633ce8fb9f87dp+9) {
+        const double w = exp_glibc(0.5 * ax, tab);
+        const double t = 0.5 * w;
+        return t * w;
+    }
+    return __longlong_as_double(0x7ff0000000000000LL);
+}
+
+// Integrand ids (include/aquad.h aq_integrand).
+enum : int { F_COSH4 = 0, F_SIN_RECIP = 1 };
+
+// F(arg) exactly as the reference macro expands (aquadPartA.c:46): ((c*c)*c)*c.
+template <int FID>
+__device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict__ tab) {
+    if constexpr (FID == F_COSH4) {
+        const double c = cosh_glibc(x, tab);
+        return c * c * c * c;
+    } else {
+        // SURVEY config 4: sin(1/x). Leaf counts are insensitive to +-1 ulp in sin,
+        // so the device libm's faithful sin is used.
+        return sin(1.0 / x);
+    }
+}
+
+// Stage the exp table into LDS (call from every thread, then __syncthreads()).
+__device__ __forceinline__ void stage_exp_table(ExpEntry* lds, const ExpEntry* __restrict__ g) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) lds[i] = g[i];
+}
+
+}  // namespace aq

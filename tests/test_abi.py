@@ -1,0 +1,87 @@
+"""The C-ABI boundary (include/aquad.h) without a GPU: the library builds, loads, exports every
+declared symbol, and the host-side observable surface matches the reference's."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "aquad.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(aq_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ppls_amd import _lib
+    return _lib.load()
+
+
+def test_header_declares_expected_api():
+    fns = header_functions()
+    from ppls_amd import _lib
+    assert fns == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing
+    out = subprocess.run(["nm", "-D", "--defined-only", lib._name], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (aq_[a-z0-9_]+)$", out, flags=re.M))
+    assert set(header_functions()) <= exported
+
+
+def test_library_is_gfx950_code_object(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", lib._name], capture_output=True, text=True)
+    assert ".hip_fatbin" in out.stdout
+    blob = open(lib._name, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_strerror_and_arg_validation(lib):
+    import ctypes
+    assert lib.aq_strerror(0) == b"ok"
+    assert lib.aq_strerror(-5) == b"maximum refinement depth reached"
+    # NULL context / arguments are rejected before any device call
+    assert lib.aq_integrate(None, None, None) == -1
+    assert lib.aq_fetch(None, 0, None) == -1
+    n = ctypes.c_int(-1)
+    rc = lib.aq_device_count(ctypes.byref(n))
+    assert (rc == 0) == (n.value > 0)
+
+
+def test_cli_numprocs_error_matches_reference():
+    """aquadPartA.c:86-90: numprocs < 2 -> that exact stderr line and exit(1)."""
+    from ppls_amd import build
+    build.build()
+    p = subprocess.run([build.CLI, "-n", "1"], capture_output=True, text=True)
+    assert p.returncode == 1
+    assert p.stderr == "ERROR: Must have at least 2 processes to run\n"
+    assert p.stdout == ""
+
+
+def test_python_farmer_numprocs_error():
+    from ppls_amd import AquadError, farmer
+    with pytest.raises(AquadError, match="ERROR: Must have at least 2 processes to run"):
+        farmer(1)
+
+
+@pytest.mark.parametrize("name", ["cosh4_eps1e-3", "cosh4_eps1e-10", "sin_recip_eps1e-9"])
+def test_format_reference_is_byte_identical(trees, name):
+    """main()'s printout (aquadPartA.c:107-117) for the reference's own numbers."""
+    from ppls_amd import format_reference
+    ref = trees[name]["reference"]
+    area = float(ref["area_printed"])
+    assert format_reference(area, ref["tasks_per_process"]) == ref["stdout"]
+
+
+def test_group_tasks_deals_cus_round_robin():
+    from ppls_amd.aquad import group_tasks
+    assert group_tasks({5: 1, 1: 10, 9: 100}, 2) == [10 + 100, 1]
+    assert sum(group_tasks({i: i for i in range(256)}, 4)) == sum(range(256))

@@ -1,0 +1,183 @@
+"""GPU parity: the HIP engine (through the C ABI, include/aquad.h) against the oracle and the
+reference's golden vectors. Bar: interval counts (tasks, accepted, per-level histograms) bit-exact;
+area within 1e-12 relative of the quad-precision Σ of leaf areas (BASELINE.json north_star);
+device cosh bit-identical to host glibc 2.35."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+AREA_RTOL = 1e-12  # BASELINE.json north_star: "its area to a stated relative tolerance of 1e-12"
+
+TREE_CASES = ["cosh4_eps1e-3", "cosh4_eps1e-6", "cosh4_eps1e-8", "cosh4_eps1e-10", "cosh4_eps1e-12",
+              "sin_recip_eps1e-9", "cosh4_eps1e3_root_leaf", "cosh4_empty_interval", "cosh4_neg_domain"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from ppls_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _problem(g):
+    from ppls_amd import Problem
+    return Problem(0 if g["integrand"] == "cosh4" else 1, g["a"], g["b"], g["eps"])
+
+
+def _area_ok(got, quad_str):
+    want = float(quad_str)
+    if want == 0.0:
+        return got == 0.0
+    return abs(got - want) <= AREA_RTOL * abs(want)
+
+
+def test_native_library_is_loaded(ctx):
+    from ppls_amd import _lib
+    maps = open("/proc/self/maps").read()
+    assert _lib.LIB_PATH in maps
+    assert ctx.num_cus > 0
+
+
+def test_device_cosh_bit_exact_fixture(ctx, libm_bits):
+    x = libm_bits["x"].view(np.float64)
+    got = ctx.eval_cosh(x).view(np.uint64)
+    bad = np.nonzero(got != libm_bits["cosh"])[0]
+    assert bad.size == 0, [(float(x[i]), hex(int(got[i])), hex(int(libm_bits['cosh'][i]))) for i in bad[:10]]
+
+
+def test_device_cosh_bit_exact_random(ctx, oracle):
+    rng = np.random.default_rng(11)
+    x = np.concatenate([rng.uniform(0.0, 5.0, 2_000_000), rng.uniform(0.0, 0.35, 200_000),
+                        rng.uniform(5.0, 30.0, 100_000), -rng.uniform(0.0, 5.0, 100_000)])
+    got = ctx.eval_cosh(x).view(np.uint64)
+    want = oracle.cosh(x).view(np.uint64)  # restated glibc (pinned to libm by test_oracle)
+    assert int((got != want).sum()) == 0
+
+
+def test_device_integrand_bit_exact(ctx, oracle):
+    rng = np.random.default_rng(12)
+    x = rng.uniform(0.0, 5.0, 500_000)
+    want = np.array([oracle.F(v) for v in x[:20000]])
+    got = ctx.eval_integrand(x[:20000])
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_device_sin_recip_faithful(ctx, oracle):
+    rng = np.random.default_rng(13)
+    x = rng.uniform(1e-4, 1.0, 20000)
+    got = ctx.eval_integrand(x, integrand=1)
+    want = np.sin(1.0 / x)
+    ulps = np.abs(got.view(np.int64) - want.view(np.int64))
+    assert ulps.max() <= 1
+
+
+@pytest.mark.parametrize("name", TREE_CASES)
+def test_persistent_tree_parity(ctx, trees, name):
+    g = trees[name]
+    r = ctx.integrate(_problem(g))
+    assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"])
+    assert r.tasks_per_level == g["tasks_per_level"]
+    assert r.leaves_per_level == g["leaves_per_level"]
+    assert _area_ok(r.area, g["area_quad"]), (r.area, g["area_quad"])
+    assert sum(r.tasks_per_cu.values()) == r.tasks
+    assert r.n_cu == len(r.tasks_per_cu) >= 1
+
+
+@pytest.mark.parametrize("name", ["cosh4_eps1e-3", "cosh4_eps1e-8", "cosh4_eps1e-10", "sin_recip_eps1e-9",
+                                  "cosh4_eps1e3_root_leaf", "cosh4_empty_interval", "cosh4_neg_domain"])
+def test_level_path_parity(ctx, trees, name):
+    g = trees[name]
+    r = ctx.integrate_levels(_problem(g))
+    assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"])
+    assert r.tasks_per_level == g["tasks_per_level"]
+    assert r.leaves_per_level == g["leaves_per_level"]
+    assert _area_ok(r.area, g["area_quad"])
+
+
+def test_reference_known_answer_printout(ctx, trees):
+    """aquadPartA.c:31-32: Area=7583461.801486 at EPSILON=1e-3; Σ tasks = 6567."""
+    from ppls_amd import farmer, format_reference
+    area, tpp = farmer(5, ctx=ctx)
+    out = format_reference(area, tpp)
+    ref = trees["cosh4_eps1e-3"]["reference"]["stdout"]
+    assert out.splitlines()[0] == ref.splitlines()[0] == "Area=7583461.801486"
+    assert out.splitlines()[2:4] == ref.splitlines()[2:4]
+    assert tpp[0] == 0 and sum(tpp) == 6567 and len(tpp) == 5
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+@pytest.mark.parametrize("name", ["cosh4_eps1e-10", "sin_recip_eps1e-9"])
+def test_shards_match_oracle_partition(ctx, trees, oracle, name, nshards):
+    g = trees[name]
+    p = _problem(g)
+    tot_t = tot_l = 0
+    area = 0.0
+    for s in range(nshards):
+        r = ctx.integrate_shard(p, s, nshards)
+        o = oracle.integrate_shard(s, nshards, G=ctx.num_cus, integrand=p.integrand, a=p.a, b=p.b, eps=p.eps)
+        assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
+        assert r.tasks_per_level == o.tasks_per_level
+        tot_t += r.tasks
+        tot_l += r.accepted
+        area += r.area
+    assert (tot_t, tot_l) == (g["tasks"], g["leaves"])
+    assert _area_ok(area, g["area_quad"])
+
+
+def test_async_slots_back_to_back(ctx, trees):
+    from ppls_amd import Problem
+    g = trees["cosh4_eps1e-10"]
+    k = 12
+    for s in range(k):
+        ctx.integrate_async(Problem(eps=1e-10), s)
+    ctx.synchronize()
+    for s in range(k):
+        r = ctx.fetch(s)
+        assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"])
+        assert _area_ok(r.area, g["area_quad"])
+
+
+def test_repeatable_counts(ctx, trees):
+    from ppls_amd import Problem
+    g = trees["cosh4_eps1e-12"]
+    for _ in range(3):
+        r = ctx.integrate(Problem(eps=1e-12))
+        assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"])
+
+
+def test_errors(ctx):
+    from ppls_amd import AquadError, Problem
+    with pytest.raises(AquadError):
+        ctx.integrate(Problem(a=1.0, b=0.0))
+    with pytest.raises(AquadError):
+        ctx.integrate(Problem(eps=float("nan")))
+    with pytest.raises(AquadError, match="depth"):
+        ctx.integrate(Problem(eps=1e-10, max_depth=10))
+    # the context is still usable after an error
+    assert ctx.integrate(Problem(eps=1e-3)).tasks == 6567
+
+
+def test_batch_front_end(ctx, batch_golden, oracle):
+    a, b = oracle.batch_bounds(64)
+    area, tasks, acc = ctx.integrate_batch(a, b, 1e-3)
+    assert [int(v) for v in acc] == batch_golden["leaves_eps1e-3_first256"][:64]
+    assert (tasks == 2 * acc - 1).all()
+    want = np.array([float.fromhex(h) for h in batch_golden["area_eps1e-3_first256_hex"][:64]])
+    assert np.all(np.abs(area - want) <= AREA_RTOL * np.abs(want))
+
+
+def test_cli_reference_output(trees):
+    from ppls_amd import build
+    build.build()
+    out = subprocess.run([build.CLI, "-n", "5"], capture_output=True, text=True, timeout=120, check=True).stdout
+    lines = out.splitlines()
+    assert lines[0] == "Area=7583461.801486"
+    assert lines[2] == "Tasks Per Process"
+    assert lines[3] == "0\t1\t2\t3\t4\t"
+    counts = [int(v) for v in lines[4].split()]
+    assert counts[0] == 0 and sum(counts) == 6567

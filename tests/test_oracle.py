@@ -1,0 +1,129 @@
+"""The CPU oracle (oracle/aq_oracle.c) against the reference's golden vectors.
+
+Pins: (1) the reference's header known answer (aquadPartA.c:31-36: Area=7583461.801486, 6567
+tasks); (2) stdout of the reference binary compiled from /root/reference by oracle/Makefile
+(recorded in tests/golden/trees.json by tests/golden/make_golden.py); (3) host glibc 2.35 libm
+bit patterns (tests/golden/libm_bits.npz).
+"""
+import os
+import platform
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def test_header_known_answer(oracle):
+    # aquadPartA.c:31-36: mpirun -c 5 -> Area=7583461.801486, tasks 0 1679 1605 1682 1601 (sum 6567)
+    r = oracle.integrate(eps=1e-3)
+    assert "%f" % r.area == "7583461.801486"
+    assert "%f" % r.area_lifo == "7583461.801486"
+    assert r.tasks == 1679 + 1605 + 1682 + 1601
+    assert r.leaves == (r.tasks + 1) // 2
+
+
+@pytest.mark.parametrize("name", ["cosh4_eps1e-3", "cosh4_eps1e-6", "cosh4_eps1e-8", "cosh4_eps1e-10",
+                                  "sin_recip_eps1e-9", "cosh4_eps1e3_root_leaf", "cosh4_empty_interval",
+                                  "cosh4_neg_domain"])
+def test_oracle_tree_fixture(oracle, trees, name):
+    g = trees[name]
+    f = oracle.COSH4 if g["integrand"] == "cosh4" else oracle.SIN_RECIP
+    r = oracle.integrate(f, g["a"], g["b"], g["eps"])
+    assert r.tasks == g["tasks"] and r.leaves == g["leaves"] and r.levels == g["levels"]
+    assert r.tasks_per_level == g["tasks_per_level"]
+    assert r.leaves_per_level == g["leaves_per_level"]
+    assert r.area_quad_str == g["area_quad"]
+    assert float(r.area_lifo).hex() == g["area_lifo_hex"]
+
+
+@pytest.mark.parametrize("name", ["cosh4_eps1e-3", "cosh4_eps1e-10", "cosh4_eps1e-12", "sin_recip_eps1e-9"])
+def test_fixture_matches_reference_stdout(trees, name):
+    """The restatement's numbers are the reference binary's own output (recorded verbatim)."""
+    g = trees[name]
+    ref = g["reference"]
+    assert ref["tasks_total"] == g["tasks"]
+    assert ref["tasks_per_process"][0] == 0
+    assert ref["area_printed"] == "%f" % float.fromhex(g["area_lifo_hex"]) or ref["area_printed"] == \
+        "%f" % float(g["area_quad"])
+    assert "%f" % float(g["area_quad"]) == ref["area_printed"]
+    p2 = g["reference_p2"]
+    assert p2["area_printed"] == g["area_lifo_printed"]  # one worker = LIFO order exactly
+    assert p2["tasks_per_process"] == [0, g["tasks"]]
+
+
+def test_fixture_histogram_consistency(trees):
+    for name, g in trees.items():
+        assert sum(g["tasks_per_level"]) == g["tasks"], name
+        assert sum(g["leaves_per_level"]) == g["leaves"], name
+        if g["tasks"]:
+            assert g["tasks"] == 2 * g["leaves"] - 1, name
+        # a level's tasks are the previous level's refined tasks times two
+        for d in range(1, len(g["tasks_per_level"])):
+            assert g["tasks_per_level"][d] == 2 * (g["tasks_per_level"][d - 1] - g["leaves_per_level"][d - 1])
+
+
+def test_oracle_cosh_bits_fixture(oracle, libm_bits):
+    x = libm_bits["x"].view(np.float64)
+    got = oracle.cosh(x).view(np.uint64)
+    assert np.array_equal(got, libm_bits["cosh"])
+    ex = libm_bits["exp_x"].view(np.float64)
+    assert np.array_equal(oracle.exp(ex).view(np.uint64), libm_bits["exp"])
+
+
+def _host_is_glibc_235():
+    try:
+        return platform.libc_ver()[1] == "2.35"
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(not _host_is_glibc_235(), reason="host libm is not glibc 2.35")
+def test_oracle_vs_host_libm_random(oracle):
+    rng = np.random.default_rng(7)
+    x = rng.uniform(0.0, 5.0, 1_000_000)
+    assert np.array_equal(oracle.cosh(x).view(np.uint64), oracle.cosh(x, oracle.HOST_LIBM).view(np.uint64))
+    xs = rng.uniform(2.0 ** -54, 0.34657359027997264, 200_000)  # |x| < 0.5 ln2: cosh's expm1 range
+    assert np.array_equal(oracle.expm1(xs).view(np.uint64), oracle.expm1(xs, oracle.HOST_LIBM).view(np.uint64))
+    big = rng.uniform(0.35, 700.0, 200_000)
+    assert np.array_equal(oracle.exp(big).view(np.uint64), oracle.exp(big, oracle.HOST_LIBM).view(np.uint64))
+
+
+def test_exp_tables_agree():
+    """Oracle table (mpmath) == product table (decimal): two independent generators of glibc's data."""
+    a = re.findall(r"0x[0-9a-f]{16}", open(os.path.join(ROOT, "oracle", "glibc_exp_table.h")).read())
+    b = re.findall(r"0x[0-9a-f]{16}", open(os.path.join(ROOT, "ppls_amd", "csrc", "aq_exp_table.h")).read())
+    assert len(a) == 256 and a == b
+
+
+def test_shard_partition_sums_to_total(oracle):
+    tot = oracle.integrate(eps=1e-8)
+    for n in (1, 2, 3, 4, 8):
+        parts = [oracle.integrate_shard(s, n, G=256, eps=1e-8) for s in range(n)]
+        assert sum(p.tasks for p in parts) == tot.tasks
+        assert sum(p.leaves for p in parts) == tot.leaves
+        assert max(p.levels for p in parts) == tot.levels
+        assert [sum(col) for col in zip(*[p.tasks_per_level + [0] * (tot.levels - p.levels) for p in parts])] == \
+            tot.tasks_per_level
+        assert abs(sum(p.area for p in parts) - tot.area) <= 1e-13 * tot.area
+
+
+@pytest.mark.parametrize("G", [1, 7, 64, 304])
+def test_shard_partition_any_grid(oracle, G):
+    tot = oracle.integrate(oracle.SIN_RECIP, 1e-4, 1.0, 1e-6)
+    parts = [oracle.integrate_shard(s, 2, G=G, integrand=oracle.SIN_RECIP, a=1e-4, b=1.0, eps=1e-6)
+             for s in range(2)]
+    assert sum(p.tasks for p in parts) == tot.tasks and sum(p.leaves for p in parts) == tot.leaves
+
+
+def test_batch_bounds_and_kat(oracle, batch_golden):
+    a, b = oracle.batch_bounds(10000)
+    assert [[float(x).hex(), float(y).hex()] for x, y in zip(a[:16], b[:16])] == batch_golden["first_bounds_hex"]
+    assert (a <= b).all() and (a >= 0).all() and (b < 5).all()
+    ar, t, lv = oracle.integrate_batch(a[:256], b[:256], 1e-3)
+    assert [int(v) for v in lv] == batch_golden["leaves_eps1e-3_first256"]
+    assert [float(v).hex() for v in ar] == batch_golden["area_eps1e-3_first256_hex"]
+    assert (t == 2 * lv - 1).all()
+    # SURVEY §8d KAT: first 10 000 draws -> mean leaves 711.5 at eps=1e-3
+    assert abs(batch_golden["mean_leaves_eps1e-3"] - 711.5) < 0.05
