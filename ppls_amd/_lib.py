@@ -16,6 +16,7 @@ EXPORTS = (
     "aq_integrate", "aq_integrate_shard", "aq_async_slots", "aq_integrate_async", "aq_fetch",
     "aq_synchronize", "aq_gather_results", "aq_integrate_levels", "aq_level_histogram", "aq_tasks_per_cu",
     "aq_integrate_batch", "aq_eval_integrand", "aq_eval_cosh", "aq_kernel_timing", "aq_kernel_time",
+    "aq_set_diagnostics", "aq_diagnostics",
     "aq_print_reference",
 )
 
@@ -72,6 +73,8 @@ def load(build_if_missing=True):
         "aq_eval_cosh": ([vp, ctypes.c_size_t, dp, dp], ctypes.c_int),
         "aq_kernel_timing": ([vp, ctypes.c_int], ctypes.c_int),
         "aq_kernel_time": ([vp, dp, up], ctypes.c_int),
+        "aq_set_diagnostics": ([vp, ctypes.c_int], ctypes.c_int),
+        "aq_diagnostics": ([vp, up, ctypes.c_int], ctypes.c_int),
         "aq_print_reference": ([vp, ctypes.c_double, up, ctypes.c_int], None),
     }
     for name, (args, res) in sig.items():

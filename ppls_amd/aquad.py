@@ -174,6 +174,23 @@ class Context:
         _check(self.L.aq_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), "aq_kernel_time")
         return ms.value, n.value
 
+    DIAG_FIELDS = ("t_start", "t_seeded", "t_first_idle", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
+                   "records_out", "t_produce", "t_idle", "seeds", "pool_push", "cu", "records_in", "active_lanes",
+                   "c_round", "c_eval", "pool_take", "lock_spins", "c_lead", "spill_records", "max_ring", "c_seed")
+    DIAG_WORDS = 24
+
+    def set_diagnostics(self, enable: bool):
+        _check(self.L.aq_set_diagnostics(self._h, 1 if enable else 0), "aq_set_diagnostics")
+
+    def diagnostics(self):
+        """Per-workgroup timeline of the last persistent launch: numpy (n_wg, 16) uint64 + field names."""
+        w = self.DIAG_WORDS
+        out = np.zeros(w * 2048, np.uint64)
+        n = self.L.aq_diagnostics(self._h, _up(out), out.size)
+        if n < 0:
+            _check(n, "aq_diagnostics")
+        return out[:w * n].reshape(n, w), self.DIAG_FIELDS
+
     # -- batch / libm ------------------------------------------------------------------------
     def integrate_batch(self, a, b, eps, integrand=COSH4):
         a = np.ascontiguousarray(a, np.float64)

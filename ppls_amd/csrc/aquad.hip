@@ -62,11 +62,12 @@ enum : unsigned { ERRB_TIMEOUT = 1, ERRB_OVERFLOW = 2, ERRB_DEPTH = 4 };
 // Persistent-path control block (one per context). Valid between launches: the last workgroup
 // of every launch publishes the totals into the launch's SlotOut and resets this block, so a
 // launch needs no memset in front of it (each memset would be one more dispatch per integral).
+struct alignas(128) Line { unsigned v; unsigned pad[31]; };
 struct Ctl {
-    unsigned q_tail;           // chunk slots claimed by producers
-    unsigned q_head;           // tickets taken by idle workgroups
-    int q_tokens;              // busy workgroups + records in published, unconsumed chunks (= G at launch)
-    unsigned exited;           // workgroups that have flushed their accumulators
+    Line q_tail;               // chunk slots claimed by producers
+    Line q_head;               // tickets taken by idle workgroups
+    Line q_tokens;             // busy workgroups + records in published, unconsumed chunks (= G at launch)
+    Line exited;               // workgroups that have flushed their accumulators
     double area;
     unsigned long long tasks;
     unsigned long long leaves;
@@ -257,24 +258,78 @@ __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsig
 
 // ------------------------------------------------------------------------------------------------
 // Persistent on-device farmer.
+//
+// Work unit = an interval record {l, r, F(l), F(r), depth}. Worker = a WAVEFRONT: each of the NW
+// waves of a workgroup owns a ring of WCAP records in LDS and runs rounds of "pop <= 64 records,
+// evaluate F(mid) for each (aquadPartA.c:183-191), push the children (:192-197) with a ballot /
+// mbcnt compaction" with no workgroup barrier at all. Waves share work through a locked LDS pool
+// (overflow in, idle waves out); workgroups share work through an HBM ticket queue driven by one
+// elected leader wave per workgroup.
 // ------------------------------------------------------------------------------------------------
-constexpr int PT = 512;             // threads per workgroup (8 waves, 2 per SIMD)
-constexpr int PW = PT / 64;         // waves per workgroup
-constexpr int CAP = 4096;           // LDS ring capacity, records (power of two)
-constexpr int CMASK = CAP - 1;
+constexpr int PT = 512;             // threads per workgroup
+constexpr int NW = PT / 64;         // waves (workers) per workgroup: 8, two per SIMD
+constexpr int WCAP = 256;           // per-wave LDS ring, records (power of two)
+constexpr int PCAP = 2048;          // per-workgroup LDS pool ring, records (power of two)
+constexpr int LREC = NW * WCAP + PCAP;   // LDS record slots: 4096 x 33 B = 132 KiB
+constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = 512;             // records per HBM queue chunk
 constexpr int S_POS = 5;            // 2^S_POS seed positions per virtual worker (32..63 dealt)
-constexpr int DONATE_MIN = 64;      // a busy workgroup donates only from stacks at least this deep
+constexpr int GIVE_MIN = 96;        // a busy wave feeds the pool for idle siblings only above this depth
+constexpr int DONATE_MIN = 128;     // records needed before a workgroup donates to another CU
+constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
+
+// Write-through (sc1) global accesses for the chunk hand-off: the producer stores every payload
+// byte sc1 and drains vmcnt before one lane's sc1 flag store; the consumer polls the flag and
+// reads the payload with sc1 loads only (MI355X_MICROARCH.md, "Valid forms", row 1) -- no
+// release / acquire fences, whose L2 write-back / invalidate cost microseconds.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ unsigned ld_wt(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_add(int* p, int v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned g_add(unsigned* p, unsigned v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned g_ld(unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Diagnostics record per workgroup (aq_set_diagnostics): realtime stamps are s_memrealtime ticks
+// (100 MHz); cycle counts are s_memtime shader cycles measured by wave 0.
+enum : int {
+    DG_T_START = 0, DG_T_SEEDED, DG_T_FIRST_IDLE, DG_T_EXIT, DG_ROUNDS, DG_TASKS, DG_CHUNKS_OUT, DG_CHUNKS_IN,
+    DG_RECORDS_OUT, DG_T_PRODUCE, DG_T_IDLE, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
+    DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_C_LEAD, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
+    DIAG_WORDS = 24
+};
+
+__device__ __forceinline__ unsigned long long clk() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    return t;
+}
 
 struct Chunk {                      // SoA, one queue slot
     double l[CH], r[CH], fl[CH], fr[CH];
-    unsigned char d[CH];
+    unsigned d[CH];
     unsigned count;
-    unsigned pad[15];
+    unsigned pad[31];
 };
 
 struct PersistParams {
-    double a, b, eps, fa_unused;
+    double a, b, eps, pad0;
     int max_depth;
     int shard, nshards;
     int D;                          // seed depth
@@ -283,6 +338,7 @@ struct PersistParams {
     unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
     Ctl* ctl;
     SlotOut* out;
+    unsigned long long* diag;          // optional per-workgroup timeline (DIAG_WORDS each), or null
     Chunk* chunks;
     unsigned* ready;
     const ExpEntry* gtab;
@@ -290,24 +346,94 @@ struct PersistParams {
 
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
 
-template <int FID, bool HIST>
+// Shared (LDS) state of one workgroup.
+struct WgState {
+    int lock;            // pool lock (lane 0 of the holding wave)
+    unsigned pbot, ptop; // pool ring, monotonic indices
+    int idle;            // waves with no records that are counted idle
+    int phase;           // 0 running, 1 a leader wave is at the HBM queue, 2 exit
+    int busy_token;      // the workgroup holds one token of the HBM-queue protocol
+    int err;
+    int pad;
+    unsigned top0[NW];   // seeded ring tops
+};
+
+// LDS record arrays (SoA), one per field.
+struct LdsRecs {
+    double* l;
+    double* r;
+    double* fl;
+    double* fr;
+    unsigned char* d;
+};
+
+__device__ __forceinline__ void wave_lock(int* lock, unsigned lane, unsigned long long& spins) {
+    if (lane == 0) {
+        int expect = 0;
+        while (!__hip_atomic_compare_exchange_strong(lock, &expect, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            expect = 0;
+            ++spins;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void wave_unlock(int* lock, unsigned lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) __hip_atomic_store(lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Copy one record (LDS slot i -> LDS slot j).
+__device__ __forceinline__ void copy_rec(const LdsRecs& R, unsigned i, unsigned j) {
+    const double l = R.l[i], r = R.r[i], fl = R.fl[i], fr = R.fr[i];
+    const unsigned char d = R.d[i];
+    R.l[j] = l; R.r[j] = r; R.fl[j] = fl; R.fr[j] = fr; R.d[j] = d;
+}
+
+// Publish k records (LDS slots src(i), i < k, i.e. base..) as HBM chunk `slot` (caller: one whole wave).
+template <typename SrcIdx>
+__device__ __forceinline__ void publish_chunk(const PersistParams& P, const LdsRecs& R, unsigned slot, unsigned k,
+                                              SrcIdx src, unsigned lane) {
+    Chunk* __restrict__ c = P.chunks + slot;
+    for (unsigned i = lane; i < k; i += 64) {
+        const unsigned j = src(i);
+        st_wt(&c->l[i], R.l[j]); st_wt(&c->r[i], R.r[j]); st_wt(&c->fl[i], R.fl[j]);
+        st_wt(&c->fr[i], R.fr[j]); st_wt(&c->d[i], (unsigned)R.d[j]);
+    }
+    if (lane == 0) st_wt(&c->count, k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the single storing wave drains
+    if (lane == 0) st_wt(&P.ready[slot], P.epoch);
+}
+
+template <int FID, bool HIST, bool DIAG>
 __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
-    __shared__ double s_l[CAP], s_r[CAP], s_fl[CAP], s_fr[CAP];
-    __shared__ unsigned char s_d[CAP];
+    __shared__ double s_l[LREC], s_r[LREC], s_fl[LREC], s_fr[LREC];
+    __shared__ unsigned char s_d[LREC];
     __shared__ ExpEntry tab[128];
-    __shared__ unsigned s_wcnt[PW];
-    __shared__ int s_cmd[4];
-    __shared__ double s_red[PW];
-    __shared__ unsigned s_redu[3][PW];
+    __shared__ WgState S;
+    __shared__ double s_red[NW];
+    __shared__ unsigned s_redu[3][NW];
+    __shared__ unsigned long long s_spill[NW];
     __shared__ unsigned s_hist[HIST ? 2 * AQ_MAX_LEVELS : 1];
 
     const unsigned tid = threadIdx.x;
     const unsigned lane = lane_id();
     const unsigned wid = tid >> 6;
     Ctl* __restrict__ ctl = P.ctl;
+    const LdsRecs R{s_l, s_r, s_fl, s_fr, s_d};
+    const unsigned long long t_entry = rtc();
+    const unsigned long long c_entry = DIAG ? clk() : 0ull;
+    unsigned long long dg[DIAG ? DIAG_WORDS : 1] = {};  // wave 0's diagnostics (DIAG builds only)
     stage_exp_table(tab, P.gtab);
     if (HIST)
         for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) s_hist[i] = 0;
+    if (tid == 0) {
+        S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1; S.err = 0;
+    }
 
     const double eps = P.eps;
     const int max_depth = P.max_depth;
@@ -315,268 +441,409 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
     unsigned my_tasks = 0, my_leaves = 0, my_maxd = 0;
     unsigned err = 0;
 
-    // ---------------- seeding: path walk to this worker's depth-D positions ----------------
+    // ---------------- seeding: this worker's depth-D positions, all F evaluations in one pass ----
+    // Virtual worker vwg of V owns positions j = k*V + (k odd ? V-1-vwg : vwg) < 2^D (snake order
+    // over bands). Every ancestor of every position is a task; its decision is the reference's
+    // arithmetic on (l, r, F(l), F(r), F(mid)), all of which are F at mids of the position's own
+    // path or at A/B. A task above depth D is counted by the owner of its leftmost descendant.
     const unsigned V = gridDim.x * (unsigned)P.nshards;
     const unsigned vwg = blockIdx.x * (unsigned)P.nshards + (unsigned)P.shard;
     const int D = P.D;
     const unsigned long long npos_total = 1ull << D;
-    const unsigned nbands = (unsigned)((npos_total + V - 1) / V);
-    // position of band k (snake order): k*V + (k odd ? V-1-vwg : vwg), valid if < 2^D
+    const unsigned nb = (unsigned)((npos_total + V - 1) / V);  // bands = positions per worker (<= 64)
+    const unsigned npairs = (unsigned)D * nb;
     auto position = [&](unsigned k, bool& valid) -> unsigned long long {
         const unsigned long long o = (k & 1u) ? (unsigned long long)(V - 1 - vwg) : (unsigned long long)vwg;
         const unsigned long long j = (unsigned long long)k * V + o;
         valid = j < npos_total;
         return j;
     };
-    double* fm = s_fl;  // F(mid) of ancestor (d, k) at fm[d*nbands + k]; stack is empty now
-    __syncthreads();
-    double fa, fb;
-    {
-        // F(A), F(B): every lane needs them in the decision pass; lane-redundant evaluation is
-        // cheaper than a broadcast round.
-        fa = integrand<FID>(P.a, tab);
-        fb = integrand<FID>(P.b, tab);
-    }
-    for (unsigned q = tid; q < (unsigned)D * nbands; q += PT) {
-        const unsigned d = q / nbands, k = q % nbands;
-        bool valid;
-        const unsigned long long p = position(k, valid);
-        double x = 0.0;
-        if (valid) {
-            const unsigned long long anc = p >> (D - (int)d);
+    // scratch in the (still empty) pool region
+    double* fm = s_l + POOL0;          // [npairs + 2]: F(mid of node (d,k)) at d*nb+k, then F(A), F(B)
+    double* leafa = s_r + POOL0;       // [npairs]: larea + rarea of node (d,k)
+    unsigned char* flag = s_d + POOL0; // [npairs]: node (d,k) refines
+    for (unsigned q = tid; q < npairs + 2; q += PT) {
+        double x;
+        if (q < npairs) {
+            const unsigned d = q / nb, k = q % nb;
+            bool valid;
+            const unsigned long long p = position(k, valid);
+            const unsigned long long anc = valid ? (p >> (D - (int)d)) : 0ull;
             double l = P.a, r = P.b;
-            for (int i = 0; i < (int)d; ++i) {
+            for (unsigned i = 0; i < d; ++i) {
                 const double m = (l + r) / 2;
                 if ((anc >> (d - 1 - i)) & 1ull) l = m; else r = m;
             }
-            x = integrand<FID>((l + r) / 2, tab);
+            x = (l + r) / 2;
+        } else {
+            x = (q == npairs) ? P.a : P.b;
         }
         fm[q] = x;
     }
+    __syncthreads();  // exp table staged
+    for (unsigned q = tid; q < npairs + 2; q += PT) fm[q] = integrand<FID>(fm[q], tab);
     __syncthreads();
-    // decision pass: wave 0, lane k = band k (nbands <= 64)
-    bool seed_alive = false;
-    double sl = 0, sr = 0, sfl = 0, sfr = 0;
+    for (unsigned q = tid; q < npairs; q += PT) {
+        const unsigned d = q / nb, k = q % nb;
+        bool valid;
+        const unsigned long long p = position(k, valid);
+        const unsigned long long anc = valid ? (p >> (D - (int)d)) : 0ull;
+        double l = P.a, r = P.b;
+        unsigned li = npairs, ri = npairs + 1;
+        for (unsigned i = 0; i < d; ++i) {
+            const double m = (l + r) / 2;
+            if ((anc >> (d - 1 - i)) & 1ull) { l = m; li = i * nb + k; } else { r = m; ri = i * nb + k; }
+        }
+        const double fl = fm[li], fr = fm[ri], fmid = fm[q];
+        const double mid = (l + r) / 2;
+        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
+        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
+        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
+        flag[q] = fabs((larea + rarea) - lrarea) > eps;      // :191
+        leafa[q] = larea + rarea;                             // :199
+    }
+    __syncthreads();
     if (wid == 0) {
         const unsigned k = lane;
         bool valid = false;
-        const unsigned long long p = (k < nbands) ? position(k, valid) : 0ull;
+        const unsigned long long p = (k < nb) ? position(k, valid) : 0ull;
         bool alive = valid;
-        double l = P.a, r = P.b, fl = fa, fr = fb;
-        for (int d = 0; d < D; ++d) {
-            if (alive) {
-                const double mid = (l + r) / 2;
-                const double fmid = fm[(unsigned)d * nbands + k];
-                const double lrarea = (fl + fr) * (r - l) / 2;
-                const double larea = (fl + fmid) * (mid - l) / 2;
-                const double rarea = (fmid + fr) * (r - mid) / 2;
-                const bool refine = fabs((larea + rarea) - lrarea) > eps;
-                const bool owner = (p & ((1ull << (D - d)) - 1ull)) == 0ull;
+        for (int d = 0; d < D && alive; ++d) {
+            const bool refine = flag[(unsigned)d * nb + k];
+            const bool owner = (p & ((1ull << (D - d)) - 1ull)) == 0ull;
+            if (owner) {
+                ++my_tasks;
+                my_maxd = max(my_maxd, (unsigned)d + 1u);
+                if (HIST) atomicAdd(&s_hist[d], 1u);
+            }
+            if (!refine) {
                 if (owner) {
-                    ++my_tasks;
-                    my_maxd = max(my_maxd, (unsigned)d + 1u);
-                    if (HIST) atomicAdd(&s_hist[d], 1u);
+                    my_area += leafa[(unsigned)d * nb + k];
+                    ++my_leaves;
+                    if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
                 }
-                if (!refine) {
-                    if (owner) {
-                        my_area += larea + rarea;
-                        ++my_leaves;
-                        if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
-                    }
-                    alive = false;
-                } else if (d + 1 >= max_depth) {
-                    if (owner) err |= ERRB_DEPTH;
-                    alive = false;
-                } else if ((p >> (D - 1 - d)) & 1ull) {
-                    l = mid;
-                    fl = fmid;
-                } else {
-                    r = mid;
-                    fr = fmid;
-                }
+                alive = false;
+            } else if (d + 1 >= max_depth) {
+                if (owner) err |= ERRB_DEPTH;
+                alive = false;
             }
         }
-        seed_alive = alive;
-        sl = l; sr = r; sfl = fl; sfr = fr;
-    }
-    __syncthreads();  // fm (aliases s_fl) fully consumed
-    unsigned top = 0, bot = 0;  // ring indices (uniform across the workgroup)
-    if (wid == 0) {
-        const unsigned long long m = __ballot(seed_alive);
-        if (seed_alive) {
-            const unsigned pos = mbcnt(m);
-            s_l[pos] = sl; s_r[pos] = sr; s_fl[pos] = sfl; s_fr[pos] = sfr;
-            s_d[pos] = (unsigned char)D;
+        double l = P.a, r = P.b, fl = 0.0, fr = 0.0;
+        if (alive) {
+            unsigned li = npairs, ri = npairs + 1;
+            for (int i = 0; i < D; ++i) {
+                const double m = (l + r) / 2;
+                if ((p >> (D - 1 - i)) & 1ull) { l = m; li = (unsigned)i * nb + k; } else { r = m; ri = (unsigned)i * nb + k; }
+            }
+            fl = fm[li];
+            fr = fm[ri];
         }
-        if (lane == 0) s_cmd[0] = (int)__popcll(m);
+        // seed k goes to wave k % NW
+        for (unsigned w = 0; w < NW; ++w) {
+            const unsigned long long m = __ballot(alive && (k % NW) == w);
+            if (alive && (k % NW) == w) {
+                const unsigned j = w * WCAP + mbcnt(m);
+                s_l[j] = l; s_r[j] = r; s_fl[j] = fl; s_fr[j] = fr; s_d[j] = (unsigned char)D;
+            }
+            if (lane == 0) S.top0[w] = (unsigned)__popcll(m);
+        }
     }
     __syncthreads();
-    top = (unsigned)s_cmd[0];
 
-    // ---------------- main loop ----------------
+    // ---------------- main loop: every wave is an independent worker ----------------
+    const unsigned base = wid * WCAP;            // this wave's ring
+    unsigned top = S.top0[wid], bot = 0;         // wave-uniform
+    if constexpr (DIAG) {
+        if (tid == 0) {
+            dg[DG_T_START] = t_entry;
+            dg[DG_T_SEEDED] = rtc();
+            dg[DG_C_SEED] = clk() - c_entry;
+            unsigned n = 0;
+            for (int w = 0; w < NW; ++w) n += S.top0[w];
+            dg[DG_SEEDS] = n;
+        }
+    }
     const unsigned long long t0 = rtc();
-    unsigned seen_head = 0, seen_tail = 0;   // thread 0 only
-    unsigned long long spilled = 0;         // thread 0 only
-    bool busy = true;                       // holds a token
-    const unsigned my_slot = cu_slot();
-    (void)my_slot;
+    bool counted_idle = false;                    // wave-uniform
+    unsigned poll_ctr = wid * (POLL_ROUNDS / NW);
+    unsigned seen_head = 0, seen_tail = 0;        // lane 0's view of the HBM queue
+    unsigned long long spilled = 0;               // records this wave sent to HBM (lane 0)
+    unsigned long long lock_spins = 0;
 
     for (;;) {
         unsigned size = top - bot;
+
         if (size == 0) {
-            // ---- idle: take a ticket, wait for a chunk or for global termination ----
-            if (tid == 0) {
-                if (busy) {
-                    __hip_atomic_fetch_add(&ctl->q_tokens, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    busy = false;
+            // ---- out of records: take from the pool, else idle / lead the workgroup to the HBM queue
+            if (counted_idle) {
+                // already counted idle: peek without the lock (the wave whose increment made every
+                // wave idle is the one that leads, so a counted wave only waits here)
+                const unsigned pt = __hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned pb = __hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int ph = __hip_atomic_load(&S.phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (pt == pb) {
+                    if (ph == 2) break;
+                    __builtin_amdgcn_s_sleep(4);
+                    continue;
                 }
-                const unsigned h = __hip_atomic_fetch_add(&ctl->q_head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                int cmd = -1;  // -1 exit, -2 error exit, else slot
+            }
+            wave_lock(&S.lock, lane, lock_spins);
+            const unsigned avail = S.ptop - S.pbot;
+            const int phase = S.phase;
+            unsigned k = 0;
+            bool lead = false;
+            if (avail > 0) {
+                k = min(avail, 64u);
+                const unsigned pb = S.pbot;
+                if (lane < k) copy_rec(R, POOL0 + ((pb + lane) & (PCAP - 1)), base + lane);
+                if (lane == 0) {
+                    S.pbot = pb + k;
+                    if (counted_idle) S.idle -= 1;
+                }
+                counted_idle = false;
+            } else {
+                if (!counted_idle) {
+                    if (lane == 0) S.idle += 1;
+                    counted_idle = true;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (phase == 0 && S.idle == NW) {   // every wave idle and the pool empty
+                    lead = true;
+                    if (lane == 0) S.phase = 1;
+                }
+            }
+            wave_unlock(&S.lock, lane);
+            if constexpr (DIAG) { if (wid == 0 && lane == 0 && k) dg[DG_POOL_TAKE] += k; }
+            if (k) {
+                bot = 0;
+                top = k;
+                continue;
+            }
+            if (phase == 2) break;
+            if (!lead) {
+                __builtin_amdgcn_s_sleep(4);
+                continue;
+            }
+            // ---- leader: this workgroup has no work; hand its token back and wait for a chunk
+            unsigned long long tl = DIAG ? rtc() : 0ull;
+            if constexpr (DIAG) { if (lane == 0 && !dg[DG_T_FIRST_IDLE]) dg[DG_T_FIRST_IDLE] = tl; }
+            int cmd = -1;   // >= 0 chunk slot, -1 exit, -2 error
+            unsigned cnt = 0;
+            if (lane == 0) {
+                if (S.busy_token) {
+                    g_add((int*)&ctl->q_tokens.v, -1);
+                    S.busy_token = 0;
+                }
+                const unsigned h = g_add(&ctl->q_head.v, 1u);
                 for (unsigned spins = 0;; ++spins) {
-                    if (h < P.qcap) {
-                        const unsigned v = __hip_atomic_load(&P.ready[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (v == P.epoch) { cmd = (int)h; break; }
+                    if (h < P.qcap && ld_wt(&P.ready[h]) == P.epoch) { cmd = (int)h; break; }
+                    if ((spins & 3u) == 0u &&
+                        __hip_atomic_load((int*)&ctl->q_tokens.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                        cmd = -1;
+                        break;
                     }
-                    const int tk = __hip_atomic_load(&ctl->q_tokens, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (tk == 0) { cmd = -1; break; }
                     if ((spins & 63u) == 63u && rtc() - t0 > P.timeout_ticks) { err |= ERRB_TIMEOUT; cmd = -2; break; }
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(8);
                 }
                 if (cmd >= 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    s_cmd[1] = (int)P.chunks[cmd].count;
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+                    cnt = ld_wt(&P.chunks[cmd].count);
                 }
-                s_cmd[0] = cmd;
             }
-            __syncthreads();
-            const int cmd = s_cmd[0];
-            if (cmd < 0) break;
-            const unsigned k = (unsigned)s_cmd[1];
+            cmd = __shfl(cmd, 0, 64);
+            cnt = __shfl(cnt, 0, 64);
+            if (cmd < 0) {
+                wave_lock(&S.lock, lane, lock_spins);
+                if (lane == 0) S.phase = 2;
+                wave_unlock(&S.lock, lane);
+                break;
+            }
+            // load the chunk into the (empty) pool, take this workgroup's token back
             const Chunk* __restrict__ c = P.chunks + cmd;
-            for (unsigned i = tid; i < k; i += PT) {
-                s_l[i] = c->l[i]; s_r[i] = c->r[i]; s_fl[i] = c->fl[i]; s_fr[i] = c->fr[i]; s_d[i] = c->d[i];
+            wave_lock(&S.lock, lane, lock_spins);
+            const unsigned pt = S.ptop;
+            for (unsigned i = lane; i < cnt; i += 64) {
+                const unsigned j = POOL0 + ((pt + i) & (PCAP - 1));
+                s_l[j] = ld_wt(&c->l[i]); s_r[j] = ld_wt(&c->r[i]); s_fl[j] = ld_wt(&c->fl[i]);
+                s_fr[j] = ld_wt(&c->fr[i]); s_d[j] = (unsigned char)ld_wt(&c->d[i]);
             }
-            bot = 0;
-            top = k;
-            if (tid == 0) {
-                // take one token for being busy, release the chunk's k record tokens
-                __hip_atomic_fetch_add(&ctl->q_tokens, 1 - (int)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                busy = true;
+            if (lane == 0) {
+                S.ptop = pt + cnt;
+                S.phase = 0;
+                S.busy_token = 1;
+                S.idle -= 1;   // the leader un-counts itself, so an empty chunk leads to a new leader
+                g_add((int*)&ctl->q_tokens.v, 1 - (int)cnt);
             }
-            __syncthreads();
+            counted_idle = false;
+            wave_unlock(&S.lock, lane);
+            if constexpr (DIAG) {
+                if (lane == 0) {
+                    dg[DG_CHUNKS_IN] += 1;
+                    dg[DG_RECORDS_IN] += cnt;
+                    dg[DG_T_IDLE] += rtc() - tl;
+                }
+            }
             continue;
         }
 
-        // ---- busy: decide whether to hand out work (spill when full, donate to waiters) ----
-        if (tid == 0) {
-            int cmd = -1;
-            unsigned k = 0;
-            if (size > (unsigned)(CAP - PT)) {
-                const unsigned s = __hip_atomic_fetch_add(&ctl->q_tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                k = min((unsigned)CH, size - (unsigned)(CAP - PT) + (unsigned)PT);
-                k = min(k, size);
-                if (s < P.qcap) cmd = (int)s; else { err |= ERRB_OVERFLOW; cmd = -3; }
-            } else if ((int)(seen_head - seen_tail) > 0 && size >= (unsigned)DONATE_MIN) {
-                unsigned expect = seen_tail;
-                if (__hip_atomic_compare_exchange_strong(&ctl->q_tail, &expect, seen_tail + 1u, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    k = min((unsigned)CH, size / 2u);
-                    if (seen_tail < P.qcap) cmd = (int)seen_tail; else { err |= ERRB_OVERFLOW; cmd = -3; }
+        // ---- keep the ring from overflowing: move its bottom 64 records to the pool, else to HBM
+        if (size > (unsigned)(WCAP - 64)) {
+            wave_lock(&S.lock, lane, lock_spins);
+            const unsigned pt = S.ptop;
+            const bool fits = (pt - S.pbot) + 64u <= (unsigned)PCAP;
+            if (fits) {
+                copy_rec(R, base + ((bot + lane) & (WCAP - 1)), POOL0 + ((pt + lane) & (PCAP - 1)));
+                if (lane == 0) S.ptop = pt + 64u;
+            }
+            wave_unlock(&S.lock, lane);
+            if (!fits) {
+                // pool full: spill 64 records to an HBM chunk (tokens first, then publish)
+                unsigned slot = 0;
+                if (lane == 0) {
+                    slot = g_add(&ctl->q_tail.v, 1u);
+                    if (slot < P.qcap) g_add((int*)&ctl->q_tokens.v, 64);
+                    spilled += 64;
+                }
+                slot = __shfl(slot, 0, 64);
+                if (slot < P.qcap) {
+                    const unsigned b = bot;
+                    publish_chunk(P, R, slot, 64u, [&](unsigned i) { return base + ((b + i) & (WCAP - 1)); }, lane);
+                } else {
+                    err |= ERRB_OVERFLOW;   // records dropped: result invalid, error reported
                 }
             }
-            if (cmd >= 0) {
-                // tokens for the k records before the chunk becomes visible
-                __hip_atomic_fetch_add(&ctl->q_tokens, (int)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                spilled += k;
-            }
-            s_cmd[2] = cmd;
-            s_cmd[3] = (int)k;
-            // refresh the queue view for the next decision (consumed at the next round's start)
-            seen_head = __hip_atomic_load(&ctl->q_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            seen_tail = __hip_atomic_load(&ctl->q_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (DIAG) { if (wid == 0 && lane == 0) dg[DG_POOL_PUSH] += 64; }
+            bot += 64;
+            continue;
         }
-        __syncthreads();
-        {
-            const int cmd = s_cmd[2];
-            const unsigned k = (unsigned)s_cmd[3];
-            if (cmd >= 0) {
-                Chunk* __restrict__ c = P.chunks + cmd;
-                for (unsigned i = tid; i < k; i += PT) {
-                    const unsigned j = (bot + i) & CMASK;
-                    c->l[i] = s_l[j]; c->r[i] = s_r[j]; c->fl[i] = s_fl[j]; c->fr[i] = s_fr[j]; c->d[i] = s_d[j];
-                }
-                if (tid == 0) c->count = k;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(&P.ready[cmd], P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                bot += k;
-                continue;  // re-evaluate size
-            } else if (cmd == -3) {
-                // queue overflow: drop records (result invalid, error reported)
+
+        // ---- feed idle sibling waves / donate to starving workgroups
+        if (size >= (unsigned)GIVE_MIN && S.idle > 0 && S.ptop == S.pbot) {
+            const unsigned k = size / 2u;   // <= 128
+            wave_lock(&S.lock, lane, lock_spins);
+            const unsigned pt = S.ptop;
+            const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
+            if (fits) {
+                for (unsigned i = lane; i < k; i += 64)
+                    copy_rec(R, base + ((bot + i) & (WCAP - 1)), POOL0 + ((pt + i) & (PCAP - 1)));
+                if (lane == 0) S.ptop = pt + k;
+            }
+            wave_unlock(&S.lock, lane);
+            if (fits) {
                 bot += k;
                 continue;
             }
         }
+        if (((++poll_ctr) % POLL_ROUNDS) == 0) {
+            // another CU waits on the HBM queue and this workgroup has plenty: donate from the pool
+            // (its oldest, i.e. shallowest, records) or from the bottom of this ring
+            unsigned slot = 0xffffffffu;
+            if (lane == 0) {
+                if ((int)(seen_head - seen_tail) > 0) {
+                    unsigned expect = seen_tail;
+                    if (__hip_atomic_compare_exchange_strong(&ctl->q_tail.v, &expect, seen_tail + 1u, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        slot = seen_tail;
+                }
+                seen_head = g_ld(&ctl->q_head.v);
+                seen_tail = g_ld(&ctl->q_tail.v);
+            }
+            slot = __shfl(slot, 0, 64);
+            if (slot != 0xffffffffu) {
+                if (slot >= P.qcap) {
+                    err |= ERRB_OVERFLOW;
+                } else {
+                    wave_lock(&S.lock, lane, lock_spins);
+                    const unsigned pavail = S.ptop - S.pbot;
+                    unsigned k;
+                    if (pavail >= (unsigned)DONATE_MIN) {
+                        k = min((unsigned)CH, pavail / 2u);
+                        const unsigned pb = S.pbot;
+                        if (lane == 0) g_add((int*)&ctl->q_tokens.v, (int)k);
+                        publish_chunk(P, R, slot, k, [&](unsigned i) { return POOL0 + ((pb + i) & (PCAP - 1)); }, lane);
+                        if (lane == 0) S.pbot = pb + k;
+                        wave_unlock(&S.lock, lane);
+                    } else {
+                        wave_unlock(&S.lock, lane);
+                        k = size / 2u;   // may be 0: an empty chunk is harmless
+                        if (lane == 0) g_add((int*)&ctl->q_tokens.v, (int)k);
+                        const unsigned b = bot;
+                        publish_chunk(P, R, slot, k, [&](unsigned i) { return base + ((b + i) & (WCAP - 1)); }, lane);
+                        bot += k;
+                    }
+                    if (lane == 0) spilled += k;
+                    if constexpr (DIAG) {
+                        if (lane == 0) { dg[DG_CHUNKS_OUT] += 1; dg[DG_RECORDS_OUT] += k; }
+                    }
+                    continue;
+                }
+            }
+        }
 
-        // ---- one round: pop up to PT records from the top, evaluate, push children ----
-        const unsigned n = min(size, (unsigned)PT);
+        // ---- one round: pop up to 64 records from the top of this wave's ring
+        unsigned long long c0 = 0, c1 = 0;
+        if constexpr (DIAG) c0 = clk();
+        const unsigned n = min(size, 64u);
         const unsigned b0 = top - n;
+        const bool active = lane < n;
         double l = 0, r = 0, fl = 0, fr = 0;
         unsigned d = 0;
-        const bool active = tid < n;
         if (active) {
-            const unsigned j = (b0 + tid) & CMASK;
+            const unsigned j = base + ((b0 + lane) & (WCAP - 1));
             l = s_l[j]; r = s_r[j]; fl = s_fl[j]; fr = s_fr[j]; d = s_d[j];
         }
-        __syncthreads();  // popped region read before children overwrite it
         bool refine = false;
         double mid = 0, fmid = 0;
         if (active) {
-            const Step s = task_step<FID>(l, r, fl, fr, eps, tab);
-            mid = s.mid;
-            fmid = s.fmid;
+            const Step st = task_step<FID>(l, r, fl, fr, eps, tab);
+            mid = st.mid;
+            fmid = st.fmid;
             ++my_tasks;
             my_maxd = max(my_maxd, d + 1u);
             if (HIST) atomicAdd(&s_hist[d], 1u);
-            if (s.refine) {
-                if ((int)d + 1 >= max_depth) {
-                    err |= ERRB_DEPTH;
-                } else {
-                    refine = true;
-                }
+            if (st.refine) {
+                if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
+                else refine = true;
             } else {
-                my_area += s.larea + s.rarea;  // :199 -> :149
+                my_area += st.larea + st.rarea;  // :199 -> :149
                 ++my_leaves;
                 if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
             }
         }
+        if constexpr (DIAG) c1 = clk();
         const unsigned long long mask = __ballot(refine);
-        if (lane == 0) s_wcnt[wid] = (unsigned)__popcll(mask);
-        __syncthreads();
-        unsigned pre = 0, tot = 0;
-#pragma unroll
-        for (int w = 0; w < PW; ++w) {
-            const unsigned c = s_wcnt[w];
-            pre += (w < (int)wid) ? c : 0u;
-            tot += c;
-        }
         if (refine) {
-            const unsigned pos = b0 + 2u * (pre + mbcnt(mask));
-            const unsigned j0 = pos & CMASK, j1 = (pos + 1u) & CMASK;
+            const unsigned pos = b0 + 2u * mbcnt(mask);
+            const unsigned j0 = base + (pos & (WCAP - 1)), j1 = base + ((pos + 1u) & (WCAP - 1));
             const unsigned char cd = (unsigned char)(d + 1u);
             s_l[j0] = l;   s_r[j0] = mid; s_fl[j0] = fl;   s_fr[j0] = fmid; s_d[j0] = cd;  // [l,mid]  :192-194
             s_l[j1] = mid; s_r[j1] = r;   s_fl[j1] = fmid; s_fr[j1] = fr;   s_d[j1] = cd;  // [mid,r]  :195-197
         }
-        top = b0 + 2u * tot;
-        __syncthreads();
+        top = b0 + 2u * (unsigned)__popcll(mask);
+        if constexpr (DIAG) {
+            if (tid == 0) {
+                const unsigned long long c2 = clk();
+                dg[DG_ROUNDS] += 1;
+                dg[DG_ACTIVE_LANES] += n;
+                dg[DG_C_ROUND] += c2 - c0;
+                dg[DG_C_EVAL] += c1 - c0;
+                dg[DG_MAX_RING] = max(dg[DG_MAX_RING], (unsigned long long)size);
+            }
+        }
     }
 
     // ---------------- exit: flush this workgroup's accumulators ----------------
+    if constexpr (DIAG) {
+        if (tid == 0) {
+            dg[DG_T_EXIT] = rtc();
+            dg[DG_CU] = cu_slot();
+            dg[DG_LOCK_SPINS] = lock_spins;
+            dg[DG_SPILL_RECORDS] = spilled;
+            unsigned long long* o = P.diag + (size_t)blockIdx.x * DIAG_WORDS;
+            for (int i = 0; i < DIAG_WORDS; ++i)
+                if (i != DG_TASKS) o[i] = dg[i];
+        }
+    }
     const double wa = wave_sum(my_area);
     const unsigned wt = wave_sum_u(my_tasks), wl = wave_sum_u(my_leaves), wm = wave_max_u(my_maxd);
     if (lane == 0) {
@@ -584,17 +851,20 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
         s_redu[0][wid] = wt;
         s_redu[1][wid] = wl;
         s_redu[2][wid] = wm;
+        s_spill[wid] = spilled;
     }
     if (err) atomicOr(&ctl->error, err);
     __syncthreads();
     if (tid == 0) {
         double ba = 0.0;
         unsigned bt = 0, bl = 0, bm = 0;
-        for (int w = 0; w < PW; ++w) {
+        unsigned long long bs = 0;
+        for (int w = 0; w < NW; ++w) {
             ba += s_red[w];
             bt += s_redu[0][w];
             bl += s_redu[1][w];
             bm = max(bm, s_redu[2][w]);
+            bs += s_spill[w];
         }
         if (bt) {
             atomicAdd(&ctl->area, ba);
@@ -602,9 +872,10 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
             atomicAdd(&ctl->leaves, (unsigned long long)bl);
             atomicMax(&ctl->levels, bm);
         }
-        if (spilled) atomicAdd(&ctl->spilled, spilled);
+        if (bs) atomicAdd(&ctl->spilled, bs);
         P.out->wg_cu[blockIdx.x] = cu_slot();
         P.out->wg_tasks[blockIdx.x] = bt;
+        if (DIAG) P.diag[(size_t)blockIdx.x * DIAG_WORDS + DG_TASKS] = bt;
     }
     if (HIST) {
         for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) {
@@ -618,15 +889,15 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(&ctl->exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_cmd[0] = (old == gridDim.x - 1u) ? 1 : 0;
+        const unsigned old = __hip_atomic_fetch_add(&ctl->exited.v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S.pad = (old == gridDim.x - 1u) ? 1 : 0;
         if (old == gridDim.x - 1u) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
     }
     __syncthreads();
-    if (s_cmd[0]) {
+    if (S.pad) {
         SlotOut* __restrict__ o = P.out;
         if (HIST) {
             for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) {
@@ -651,10 +922,10 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
             __hip_atomic_store(&ctl->spilled, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ctl->levels, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ctl->error, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->q_tail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->q_head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->q_tokens, (int)gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->exited, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl->q_tail.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl->q_head.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((int*)&ctl->q_tokens.v, (int)gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl->exited.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -755,6 +1026,8 @@ struct aq_ctx {
     DevResults* h_lres = nullptr;      // pinned
     HostOut last;
     bool last_valid = false;
+    // diagnostics
+    unsigned long long* d_diag = nullptr;
     // timing
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
@@ -767,7 +1040,7 @@ namespace {
 
 int reset_ctl(aq_ctx* c) {
     Ctl h{};
-    h.q_tokens = c->persist_grid;
+    h.q_tokens.v = (unsigned)c->persist_grid;
     AQ_HIP(hipMemcpyAsync(c->d_ctl, &h, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
     AQ_HIP(hipStreamSynchronize(c->stream));
     return AQ_OK;
@@ -794,6 +1067,7 @@ int launch_persist(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int
     P.chunks = ctx->d_chunks;
     P.ready = ctx->d_ready;
     P.gtab = ctx->d_tab;
+    P.diag = ctx->d_diag;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (ctx->timing) {
         if (!ctx->ev_free.empty()) {
@@ -805,7 +1079,10 @@ int launch_persist(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int
         }
         AQ_HIP(hipEventRecord(ev.first, ctx->stream));
     }
-    hipLaunchKernelGGL((k_persist<FID, HIST>), dim3(G), dim3(PT), 0, ctx->stream, P);
+    if (P.diag)
+        hipLaunchKernelGGL((k_persist<FID, HIST, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
+    else
+        hipLaunchKernelGGL((k_persist<FID, HIST, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
     AQ_HIP(hipGetLastError());
     if (ctx->timing) {
         AQ_HIP(hipEventRecord(ev.second, ctx->stream));
@@ -888,7 +1165,7 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipGetDeviceProperties(&prop, device));
     c->num_cus = prop.multiProcessorCount;
     int occ = 0;
-    AQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_persist<F_COSH4, true>, PT, 0));
+    AQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_persist<F_COSH4, true, false>, PT, 0));
     if (occ < 1) {
         delete c;
         return AQ_ENODEV;
@@ -928,6 +1205,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_ready);
     (void)hipFree(c->d_lres);
+    (void)hipFree(c->d_diag);
     (void)hipFree(c->d_front[0]);
     (void)hipFree(c->d_front[1]);
     (void)hipFree(c->d_count);
@@ -945,6 +1223,29 @@ int aq_set_level_histograms(aq_ctx* c, int enable) {
     if (!c) return AQ_EINVAL;
     c->histograms = enable != 0;
     return AQ_OK;
+}
+
+int aq_set_diagnostics(aq_ctx* c, int enable) {
+    if (!c) return AQ_EINVAL;
+    AQ_HIP(hipSetDevice(c->device));
+    AQ_HIP(hipStreamSynchronize(c->stream));
+    if (enable && !c->d_diag) {
+        AQ_HIP(hipMalloc(&c->d_diag, sizeof(unsigned long long) * DIAG_WORDS * MAXG));
+        AQ_HIP(hipMemset(c->d_diag, 0, sizeof(unsigned long long) * DIAG_WORDS * MAXG));
+    } else if (!enable && c->d_diag) {
+        (void)hipFree(c->d_diag);
+        c->d_diag = nullptr;
+    }
+    return AQ_OK;
+}
+
+int aq_diagnostics(aq_ctx* c, uint64_t* out, int cap_words) {
+    if (!c || !out || !c->d_diag) return AQ_EINVAL;
+    AQ_HIP(hipSetDevice(c->device));
+    const size_t words = std::min<size_t>((size_t)cap_words, (size_t)DIAG_WORDS * c->persist_grid);
+    AQ_HIP(hipStreamSynchronize(c->stream));
+    AQ_HIP(hipMemcpy(out, c->d_diag, words * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return (int)(words / DIAG_WORDS);
 }
 
 int aq_async_slots(void) { return NSLOTS; }

@@ -1,0 +1,73 @@
+"""Per-workgroup timeline of the persistent kernel (diagnostics build path, not timed).
+
+  python tools/diag_persist.py [--eps 1e-10] [--reps 5] [--out gpurun_out/diag.json]
+Prints, for the last of `reps` integrals: phase times (us, relative to the earliest workgroup
+entry), rounds, lane occupancy, queue traffic and the per-workgroup task spread.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ppls_amd import Context, Problem  # noqa: E402
+
+
+def summarize(d, f):
+    col = {k: d[:, i].astype(np.float64) for i, k in enumerate(f)}
+    t0 = col["t_start"].min()
+    us = lambda v: (v - t0) / 100.0  # 100 MHz ticks -> us
+    s = {}
+    for k in ("t_start", "t_seeded", "t_first_idle", "t_exit"):
+        v = us(col[k])
+        s[k] = {"min": v.min(), "p50": float(np.median(v)), "max": v.max()}
+    s["rounds"] = {"min": col["rounds"].min(), "p50": float(np.median(col["rounds"])), "max": col["rounds"].max()}
+    s["lanes_per_round"] = float(col["active_lanes"].sum() / max(col["rounds"].sum(), 1))
+    busy = (col["t_first_idle"] - col["t_seeded"]) / 100.0
+    s["us_per_round_first_busy"] = float(np.median(busy / np.maximum(col["rounds"], 1)))
+    s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
+                  "sum": col["tasks"].sum()}
+    s["pool_push_w0"] = float(np.median(col["pool_push"]))
+    s["pool_take_w0"] = float(np.median(col["pool_take"]))
+    s["lock_spins_w0_max"] = col["lock_spins"].max()
+    s["spill_records"] = col["spill_records"].sum()
+    s["max_ring"] = col["max_ring"].max()
+    s["chunks_out"] = col["chunks_out"].sum()
+    s["chunks_in"] = col["chunks_in"].sum()
+    s["records_moved"] = col["records_out"].sum()
+    s["t_produce_us_total"] = col["t_produce"].sum() / 100.0
+    s["t_idle_us_p50"] = float(np.median(col["t_idle"])) / 100.0
+    s["seeds"] = {"min": col["seeds"].min(), "max": col["seeds"].max()}
+    r = np.maximum(col["rounds"], 1)
+    for k in ("c_round", "c_eval"):
+        s["cyc_per_round_" + k[2:]] = float(np.median(col[k] / r))
+    s["cyc_seed_p50"] = float(np.median(col["c_seed"]))
+    return s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--eps", type=float, default=1e-10)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    ctx = Context(0)
+    ctx.set_level_histograms(False)
+    ctx.set_diagnostics(True)
+    res = []
+    for _ in range(args.reps):
+        r = ctx.integrate(Problem(eps=args.eps))
+        d, f = ctx.diagnostics()
+        res.append(summarize(d, f))
+    print(json.dumps({"eps": args.eps, "tasks": r.tasks, "accepted": r.accepted, "summary": res[-1]}, indent=1,
+                     default=float))
+    if args.out:
+        np.save(args.out.replace(".json", ".npy"), d)
+        with open(args.out, "w") as fh:
+            json.dump({"eps": args.eps, "fields": f, "summaries": res}, fh, default=float, indent=1)
+
+
+if __name__ == "__main__":
+    main()
