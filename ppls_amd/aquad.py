@@ -174,9 +174,9 @@ class Context:
         _check(self.L.aq_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), "aq_kernel_time")
         return ms.value, n.value
 
-    DIAG_FIELDS = ("t_start", "t_seeded", "t_first_idle", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
-                   "records_out", "t_produce", "t_idle", "seeds", "pool_push", "cu", "records_in", "active_lanes",
-                   "c_round", "c_eval", "pool_take", "lock_spins", "c_lead", "spill_records", "max_ring", "c_seed")
+    DIAG_FIELDS = ("t_start", "t_seeded", "t_first_lead", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
+                   "records_out", "t_wait", "leads", "seeds", "pool_push", "cu", "records_in", "active_lanes",
+                   "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed")
     DIAG_WORDS = 24
 
     def set_diagnostics(self, enable: bool):

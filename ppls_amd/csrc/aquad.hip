@@ -59,38 +59,35 @@ struct DevResults {
 
 enum : unsigned { ERRB_TIMEOUT = 1, ERRB_OVERFLOW = 2, ERRB_DEPTH = 4 };
 
-// Persistent-path control block (one per context). Valid between launches: the last workgroup
-// of every launch publishes the totals into the launch's SlotOut and resets this block, so a
-// launch needs no memset in front of it (each memset would be one more dispatch per integral).
+// Persistent-path control block, one per async slot. It must be all-zero when a launch starts;
+// the host zeroes slots lazily in batches (one memset per 64 launches in sequential use) so a
+// launch needs no memset of its own. q_tokens stores (tokens - G): the HBM-queue protocol's
+// token count starts at G (every workgroup busy) and the run is over when it reaches 0.
 struct alignas(128) Line { unsigned v; unsigned pad[31]; };
 struct Ctl {
     Line q_tail;               // chunk slots claimed by producers
     Line q_head;               // tickets taken by idle workgroups
-    Line q_tokens;             // busy workgroups + records in published, unconsumed chunks (= G at launch)
-    Line exited;               // workgroups that have flushed their accumulators
-    double area;
-    unsigned long long tasks;
-    unsigned long long leaves;
-    unsigned long long spilled;
-    unsigned levels;
-    unsigned error;
-    unsigned pad[2];
+    Line q_tokens;             // tokens - G
+    Line spare;
     unsigned long long hist[2 * AQ_MAX_LEVELS];   // [0,L): tasks per level, [L,2L): accepted per level
 };
 
 constexpr int MAXG = 2048;     // max persistent workgroups per launch
-struct SlotOut {               // fully rewritten by every launch that targets the slot
+struct WgPart {                // one workgroup's share of a launch, plain stores at exit
     double area;
     unsigned long long tasks;
     unsigned long long leaves;
     unsigned long long spilled;
     unsigned levels;
     unsigned error;
+    unsigned cu;               // hardware CU slot
+    unsigned pad;
+};
+struct SlotOut {               // fully rewritten by every launch that targets the slot
     unsigned nwg;
     unsigned epoch;
-    unsigned long long hist[2 * AQ_MAX_LEVELS];
-    unsigned wg_cu[MAXG];                         // hardware CU slot of workgroup i
-    unsigned long long wg_tasks[MAXG];            // tasks evaluated by workgroup i
+    unsigned pad[2];
+    WgPart wg[MAXG];
 };
 
 // Hardware CU slot of the executing wave: xcc*256 + (se*2 + sh)*16 + cu (HW_ID / XCC_ID registers).
@@ -306,12 +303,12 @@ __device__ __forceinline__ unsigned g_ld(unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Diagnostics record per workgroup (aq_set_diagnostics): realtime stamps are s_memrealtime ticks
-// (100 MHz); cycle counts are s_memtime shader cycles measured by wave 0.
+// Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
+// realtime stamps are s_memrealtime ticks (100 MHz), cycle counts are s_memtime shader cycles.
 enum : int {
-    DG_T_START = 0, DG_T_SEEDED, DG_T_FIRST_IDLE, DG_T_EXIT, DG_ROUNDS, DG_TASKS, DG_CHUNKS_OUT, DG_CHUNKS_IN,
-    DG_RECORDS_OUT, DG_T_PRODUCE, DG_T_IDLE, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
-    DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_C_LEAD, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
+    DG_T_START = 0, DG_T_SEEDED, DG_T_FIRST_LEAD, DG_T_EXIT, DG_ROUNDS, DG_TASKS, DG_CHUNKS_OUT, DG_CHUNKS_IN,
+    DG_RECORDS_OUT, DG_T_WAIT, DG_LEADS, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
+    DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
     DIAG_WORDS = 24
 };
 
@@ -427,7 +424,10 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
     const LdsRecs R{s_l, s_r, s_fl, s_fr, s_d};
     const unsigned long long t_entry = rtc();
     const unsigned long long c_entry = DIAG ? clk() : 0ull;
-    unsigned long long dg[DIAG ? DIAG_WORDS : 1] = {};  // wave 0's diagnostics (DIAG builds only)
+    __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];  // diagnostics (DIAG builds only)
+    if (DIAG) {
+        for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
+    }
     stage_exp_table(tab, P.gtab);
     if (HIST)
         for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) s_hist[i] = 0;
@@ -507,26 +507,30 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
         const unsigned k = lane;
         bool valid = false;
         const unsigned long long p = (k < nb) ? position(k, valid) : 0ull;
+        // every flag of this position's path in one batch of independent LDS reads
+        unsigned long long fmask = 0;
+        for (int d = 0; d < D; ++d)
+            fmask |= (unsigned long long)(flag[(unsigned)d * nb + (k < nb ? k : 0)] ? 1u : 0u) << d;
+        const int dstar = (int)__builtin_ctzll(~fmask);   // first depth that does not refine (D if none)
         bool alive = valid;
-        for (int d = 0; d < D && alive; ++d) {
-            const bool refine = flag[(unsigned)d * nb + k];
-            const bool owner = (p & ((1ull << (D - d)) - 1ull)) == 0ull;
-            if (owner) {
-                ++my_tasks;
-                my_maxd = max(my_maxd, (unsigned)d + 1u);
-                if (HIST) atomicAdd(&s_hist[d], 1u);
-            }
-            if (!refine) {
+        if (valid) {
+            const int dlast = min(dstar, D - 1);
+            for (int d = 0; d <= dlast; ++d) {
+                const bool owner = (p & ((1ull << (D - d)) - 1ull)) == 0ull;
                 if (owner) {
-                    my_area += leafa[(unsigned)d * nb + k];
-                    ++my_leaves;
-                    if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
+                    ++my_tasks;
+                    my_maxd = max(my_maxd, (unsigned)d + 1u);
+                    if (HIST) atomicAdd(&s_hist[d], 1u);
+                    if (d == dstar) {
+                        my_area += leafa[(unsigned)d * nb + k];
+                        ++my_leaves;
+                        if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
+                    } else if (d + 1 >= max_depth) {
+                        err |= ERRB_DEPTH;
+                    }
                 }
-                alive = false;
-            } else if (d + 1 >= max_depth) {
-                if (owner) err |= ERRB_DEPTH;
-                alive = false;
             }
+            alive = dstar >= D && D < max_depth;
         }
         double l = P.a, r = P.b, fl = 0.0, fr = 0.0;
         if (alive) {
@@ -555,12 +559,12 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
     unsigned top = S.top0[wid], bot = 0;         // wave-uniform
     if constexpr (DIAG) {
         if (tid == 0) {
-            dg[DG_T_START] = t_entry;
-            dg[DG_T_SEEDED] = rtc();
-            dg[DG_C_SEED] = clk() - c_entry;
+            s_dg[DG_T_START] = t_entry;
+            s_dg[DG_T_SEEDED] = rtc();
+            s_dg[DG_C_SEED] = clk() - c_entry;
             unsigned n = 0;
             for (int w = 0; w < NW; ++w) n += S.top0[w];
-            dg[DG_SEEDS] = n;
+            s_dg[DG_SEEDS] = n;
         }
     }
     const unsigned long long t0 = rtc();
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
                 }
             }
             wave_unlock(&S.lock, lane);
-            if constexpr (DIAG) { if (wid == 0 && lane == 0 && k) dg[DG_POOL_TAKE] += k; }
+            if constexpr (DIAG) { if (lane == 0 && k) atomicAdd(&s_dg[DG_POOL_TAKE], (unsigned long long)k); }
             if (k) {
                 bot = 0;
                 top = k;
@@ -626,7 +630,12 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
             }
             // ---- leader: this workgroup has no work; hand its token back and wait for a chunk
             unsigned long long tl = DIAG ? rtc() : 0ull;
-            if constexpr (DIAG) { if (lane == 0 && !dg[DG_T_FIRST_IDLE]) dg[DG_T_FIRST_IDLE] = tl; }
+            if constexpr (DIAG) {
+                if (lane == 0) {
+                    atomicMin(&s_dg[DG_T_FIRST_LEAD], tl);
+                    atomicAdd(&s_dg[DG_LEADS], 1ull);
+                }
+            }
             int cmd = -1;   // >= 0 chunk slot, -1 exit, -2 error
             unsigned cnt = 0;
             if (lane == 0) {
@@ -638,7 +647,8 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
                 for (unsigned spins = 0;; ++spins) {
                     if (h < P.qcap && ld_wt(&P.ready[h]) == P.epoch) { cmd = (int)h; break; }
                     if ((spins & 3u) == 0u &&
-                        __hip_atomic_load((int*)&ctl->q_tokens.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                            __hip_atomic_load((int*)&ctl->q_tokens.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                            -(int)gridDim.x) {
                         cmd = -1;
                         break;
                     }
@@ -678,9 +688,9 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
             wave_unlock(&S.lock, lane);
             if constexpr (DIAG) {
                 if (lane == 0) {
-                    dg[DG_CHUNKS_IN] += 1;
-                    dg[DG_RECORDS_IN] += cnt;
-                    dg[DG_T_IDLE] += rtc() - tl;
+                    atomicAdd(&s_dg[DG_CHUNKS_IN], 1ull);
+                    atomicAdd(&s_dg[DG_RECORDS_IN], (unsigned long long)cnt);
+                    atomicAdd(&s_dg[DG_T_WAIT], rtc() - tl);
                 }
             }
             continue;
@@ -712,7 +722,7 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
                     err |= ERRB_OVERFLOW;   // records dropped: result invalid, error reported
                 }
             }
-            if constexpr (DIAG) { if (wid == 0 && lane == 0) dg[DG_POOL_PUSH] += 64; }
+            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_POOL_PUSH], 64ull); }
             bot += 64;
             continue;
         }
@@ -773,7 +783,10 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
                     }
                     if (lane == 0) spilled += k;
                     if constexpr (DIAG) {
-                        if (lane == 0) { dg[DG_CHUNKS_OUT] += 1; dg[DG_RECORDS_OUT] += k; }
+                        if (lane == 0) {
+                            atomicAdd(&s_dg[DG_CHUNKS_OUT], 1ull);
+                            atomicAdd(&s_dg[DG_RECORDS_OUT], (unsigned long long)k);
+                        }
                     }
                     continue;
                 }
@@ -821,61 +834,67 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
         }
         top = b0 + 2u * (unsigned)__popcll(mask);
         if constexpr (DIAG) {
-            if (tid == 0) {
+            if (lane == 0) {
                 const unsigned long long c2 = clk();
-                dg[DG_ROUNDS] += 1;
-                dg[DG_ACTIVE_LANES] += n;
-                dg[DG_C_ROUND] += c2 - c0;
-                dg[DG_C_EVAL] += c1 - c0;
-                dg[DG_MAX_RING] = max(dg[DG_MAX_RING], (unsigned long long)size);
+                atomicAdd(&s_dg[DG_ROUNDS], 1ull);
+                atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
+                atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
+                atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
+                atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)size);
+                atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
             }
         }
     }
 
-    // ---------------- exit: flush this workgroup's accumulators ----------------
-    if constexpr (DIAG) {
-        if (tid == 0) {
-            dg[DG_T_EXIT] = rtc();
-            dg[DG_CU] = cu_slot();
-            dg[DG_LOCK_SPINS] = lock_spins;
-            dg[DG_SPILL_RECORDS] = spilled;
-            unsigned long long* o = P.diag + (size_t)blockIdx.x * DIAG_WORDS;
-            for (int i = 0; i < DIAG_WORDS; ++i)
-                if (i != DG_TASKS) o[i] = dg[i];
-        }
-    }
+    // ---------------- exit: this workgroup's partial results, plain stores (no contention) ------
     const double wa = wave_sum(my_area);
     const unsigned wt = wave_sum_u(my_tasks), wl = wave_sum_u(my_leaves), wm = wave_max_u(my_maxd);
+    unsigned we = err;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) we |= (unsigned)__shfl_xor((int)we, o, 64);
     if (lane == 0) {
         s_red[wid] = wa;
         s_redu[0][wid] = wt;
         s_redu[1][wid] = wl;
         s_redu[2][wid] = wm;
-        s_spill[wid] = spilled;
+        s_spill[wid] = spilled | ((unsigned long long)we << 48);
+        if constexpr (DIAG) {
+            atomicAdd(&s_dg[DG_LOCK_SPINS], lock_spins);
+            atomicAdd(&s_dg[DG_SPILL_RECORDS], spilled);
+        }
     }
-    if (err) atomicOr(&ctl->error, err);
     __syncthreads();
     if (tid == 0) {
         double ba = 0.0;
-        unsigned bt = 0, bl = 0, bm = 0;
+        unsigned bt = 0, bl = 0, bm = 0, be = 0;
         unsigned long long bs = 0;
         for (int w = 0; w < NW; ++w) {
             ba += s_red[w];
             bt += s_redu[0][w];
             bl += s_redu[1][w];
             bm = max(bm, s_redu[2][w]);
-            bs += s_spill[w];
+            bs += s_spill[w] & 0xffffffffffffull;
+            be |= (unsigned)(s_spill[w] >> 48);
         }
-        if (bt) {
-            atomicAdd(&ctl->area, ba);
-            atomicAdd(&ctl->tasks, (unsigned long long)bt);
-            atomicAdd(&ctl->leaves, (unsigned long long)bl);
-            atomicMax(&ctl->levels, bm);
+        WgPart* o = &P.out->wg[blockIdx.x];
+        o->area = ba;
+        o->tasks = bt;
+        o->leaves = bl;
+        o->spilled = bs;
+        o->levels = bm;
+        o->error = be;
+        o->cu = cu_slot();
+        if (blockIdx.x == 0) {
+            P.out->nwg = gridDim.x;
+            P.out->epoch = P.epoch;
         }
-        if (bs) atomicAdd(&ctl->spilled, bs);
-        P.out->wg_cu[blockIdx.x] = cu_slot();
-        P.out->wg_tasks[blockIdx.x] = bt;
-        if (DIAG) P.diag[(size_t)blockIdx.x * DIAG_WORDS + DG_TASKS] = bt;
+        if constexpr (DIAG) {
+            s_dg[DG_T_EXIT] = rtc();
+            s_dg[DG_CU] = cu_slot();
+            s_dg[DG_TASKS] = bt;
+            unsigned long long* d = P.diag + (size_t)blockIdx.x * DIAG_WORDS;
+            for (int i = 0; i < DIAG_WORDS; ++i) d[i] = s_dg[i];
+        }
     }
     if (HIST) {
         for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) {
@@ -883,64 +902,47 @@ __global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
             if (v) atomicAdd(&ctl->hist[i], (unsigned long long)v);
         }
     }
-    // last workgroup out publishes the totals and resets the control block for the next launch
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old = __hip_atomic_fetch_add(&ctl->exited.v, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        S.pad = (old == gridDim.x - 1u) ? 1 : 0;
-        if (old == gridDim.x - 1u) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    if (S.pad) {
-        SlotOut* __restrict__ o = P.out;
-        if (HIST) {
-            for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) {
-                o->hist[i] = __hip_atomic_load(&ctl->hist[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ctl->hist[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (tid == 0) {
-            unsigned long long* area_bits = reinterpret_cast<unsigned long long*>(&ctl->area);
-            o->area = __longlong_as_double(
-                (long long)__hip_atomic_load(area_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            o->tasks = __hip_atomic_load(&ctl->tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o->leaves = __hip_atomic_load(&ctl->leaves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o->spilled = __hip_atomic_load(&ctl->spilled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o->levels = __hip_atomic_load(&ctl->levels, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o->error = __hip_atomic_load(&ctl->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o->nwg = gridDim.x;
-            o->epoch = P.epoch;
-            __hip_atomic_store(area_bits, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->tasks, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->leaves, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->spilled, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->levels, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->error, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->q_tail.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->q_head.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((int*)&ctl->q_tokens.v, (int)gridDim.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl->exited.v, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // Gather n slots' totals into a caller device buffer as f64 [area, tasks, accepted, error] rows,
-// ready for one collective (counts are exact in f64 below 2^53).
+// ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot sums the
+// slot's per-workgroup partials in a fixed order.
 __global__ __launch_bounds__(256) void k_gather(const SlotOut* __restrict__ slots, int first, int n, int nslots,
                                                 double* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const SlotOut& s = slots[(first + i) % nslots];
-        out[4 * i + 0] = s.area;
-        out[4 * i + 1] = (double)s.tasks;
-        out[4 * i + 2] = (double)s.leaves;
-        out[4 * i + 3] = (double)s.error;
+    __shared__ double s_a[4];
+    __shared__ unsigned long long s_t[4], s_l[4];
+    __shared__ unsigned s_e[4];
+    const SlotOut& s = slots[(first + (int)blockIdx.x) % nslots];
+    const unsigned nwg = min(s.nwg, (unsigned)MAXG);
+    double a = 0.0;
+    unsigned long long t = 0, l = 0;
+    unsigned e = 0;
+    for (unsigned i = threadIdx.x; i < nwg; i += blockDim.x) {
+        a += s.wg[i].area;
+        t += s.wg[i].tasks;
+        l += s.wg[i].leaves;
+        e |= s.wg[i].error;
+    }
+    a = wave_sum(a);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        t += __shfl_xor(t, o, 64);
+        l += __shfl_xor(l, o, 64);
+        e |= (unsigned)__shfl_xor((int)e, o, 64);
+    }
+    const unsigned w = threadIdx.x >> 6;
+    if (lane_id() == 0) { s_a[w] = a; s_t[w] = t; s_l[w] = l; s_e[w] = e; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double A = 0.0;
+        unsigned long long T = 0, L = 0;
+        unsigned E = 0;
+        for (int k = 0; k < 4; ++k) { A += s_a[k]; T += s_t[k]; L += s_l[k]; E |= s_e[k]; }
+        double* o = out + 4 * blockIdx.x;
+        o[0] = A;
+        o[1] = (double)T;
+        o[2] = (double)L;
+        o[3] = (double)E;
     }
 }
 
@@ -1006,7 +1008,8 @@ struct aq_ctx {
     bool histograms = true;
     hipStream_t stream = nullptr;
     ExpEntry* d_tab = nullptr;
-    Ctl* d_ctl = nullptr;
+    Ctl* d_ctl = nullptr;              // NSLOTS control blocks
+    bool ctl_dirty[NSLOTS] = {};       // slot's control block used since it was last zeroed
     SlotOut* d_out = nullptr;          // NSLOTS
     bool slot_hist[NSLOTS] = {};
     Chunk* d_chunks = nullptr;
@@ -1023,6 +1026,7 @@ struct aq_ctx {
     size_t eval_cap = 0;
     // host staging
     SlotOut* h_slot = nullptr;         // pinned
+    unsigned long long* h_hist = nullptr;  // pinned, 2 * AQ_MAX_LEVELS
     DevResults* h_lres = nullptr;      // pinned
     HostOut last;
     bool last_valid = false;
@@ -1038,11 +1042,13 @@ struct aq_ctx {
 
 namespace {
 
-int reset_ctl(aq_ctx* c) {
-    Ctl h{};
-    h.q_tokens.v = (unsigned)c->persist_grid;
-    AQ_HIP(hipMemcpyAsync(c->d_ctl, &h, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
-    AQ_HIP(hipStreamSynchronize(c->stream));
+// Zero the control block of `slot` (and of the following slots up to a batch of 64) if it has
+// been used since it was last zeroed: one memset per 64 launches when slots are used in order.
+int ensure_clean(aq_ctx* c, int slot) {
+    if (!c->ctl_dirty[slot]) return AQ_OK;
+    int n = 0;
+    while (slot + n < NSLOTS && n < 64) c->ctl_dirty[slot + n++] = false;
+    AQ_HIP(hipMemsetAsync(c->d_ctl + slot, 0, sizeof(Ctl) * (size_t)n, c->stream));
     return AQ_OK;
 }
 
@@ -1062,7 +1068,9 @@ int launch_persist(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int
     if (P.epoch == 0) P.epoch = ++ctx->epoch;
     P.qcap = QCAP;
     P.timeout_ticks = 100000000ull * 20ull;  // 20 s of the 100 MHz realtime clock
-    P.ctl = ctx->d_ctl;
+    int rc = ensure_clean(ctx, slot);
+    if (rc) return rc;
+    P.ctl = ctx->d_ctl + slot;
     P.out = ctx->d_out + slot;
     P.chunks = ctx->d_chunks;
     P.ready = ctx->d_ready;
@@ -1089,6 +1097,7 @@ int launch_persist(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int
         ctx->ev_pending.push_back(ev);
     }
     ctx->slot_hist[slot] = HIST;
+    ctx->ctl_dirty[slot] = true;
     return AQ_OK;
 }
 
@@ -1105,22 +1114,27 @@ void fill_result(const HostOut& h, aq_result* out) {
 }
 
 int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
-    AQ_HIP(hipMemcpyAsync(ctx->h_slot, ctx->d_out + slot, sizeof(SlotOut), hipMemcpyDeviceToHost, ctx->stream));
+    const size_t nbytes = offsetof(SlotOut, wg) + sizeof(WgPart) * (size_t)ctx->persist_grid;
+    AQ_HIP(hipMemcpyAsync(ctx->h_slot, ctx->d_out + slot, nbytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->slot_hist[slot])
+        AQ_HIP(hipMemcpyAsync(ctx->h_hist, ctx->d_ctl[slot].hist, sizeof(unsigned long long) * 2 * AQ_MAX_LEVELS,
+                              hipMemcpyDeviceToHost, ctx->stream));
     AQ_HIP(hipStreamSynchronize(ctx->stream));
     const SlotOut& s = *ctx->h_slot;
     HostOut& h = ctx->last;
     h = HostOut();
-    h.area = s.area;
-    h.tasks = s.tasks;
-    h.leaves = s.leaves;
-    h.spilled = s.spilled;
-    h.levels = s.levels;
-    h.error = s.error;
-    if (ctx->slot_hist[slot]) memcpy(h.hist, s.hist, sizeof(h.hist));
     const unsigned nwg = std::min<unsigned>(s.nwg, MAXG);
     for (unsigned i = 0; i < nwg; ++i) {
-        if (s.wg_tasks[i]) h.cu[s.wg_cu[i] % AQ_CU_SLOTS] += s.wg_tasks[i];
+        const WgPart& w = s.wg[i];
+        h.area += w.area;
+        h.tasks += w.tasks;
+        h.leaves += w.leaves;
+        h.spilled += w.spilled;
+        h.levels = std::max(h.levels, w.levels);
+        h.error |= w.error;
+        if (w.tasks) h.cu[w.cu % AQ_CU_SLOTS] += w.tasks;
     }
+    if (ctx->slot_hist[slot]) memcpy(h.hist, ctx->h_hist, sizeof(h.hist));
     ctx->last_valid = true;
     fill_result(h, out);
     return err_from_bits(h.error);
@@ -1176,18 +1190,18 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     AQ_HIP(hipMalloc(&c->d_tab, sizeof(ExpEntry) * 128));
     AQ_HIP(hipMemcpy(c->d_tab, aq_exp_tab_host, sizeof(ExpEntry) * 128, hipMemcpyHostToDevice));
-    AQ_HIP(hipMalloc(&c->d_ctl, sizeof(Ctl)));
+    AQ_HIP(hipMalloc(&c->d_ctl, sizeof(Ctl) * NSLOTS));
+    AQ_HIP(hipMemset(c->d_ctl, 0, sizeof(Ctl) * NSLOTS));
     AQ_HIP(hipMalloc(&c->d_out, sizeof(SlotOut) * NSLOTS));
     AQ_HIP(hipMemset(c->d_out, 0, sizeof(SlotOut) * NSLOTS));
     AQ_HIP(hipMalloc(&c->d_chunks, sizeof(Chunk) * (size_t)QCAP));
     AQ_HIP(hipMalloc(&c->d_ready, sizeof(unsigned) * (size_t)QCAP));
     AQ_HIP(hipMemset(c->d_ready, 0, sizeof(unsigned) * (size_t)QCAP));
     AQ_HIP(hipHostMalloc(&c->h_slot, sizeof(SlotOut), hipHostMallocDefault));
+    AQ_HIP(hipHostMalloc(&c->h_hist, sizeof(unsigned long long) * 2 * AQ_MAX_LEVELS, hipHostMallocDefault));
     AQ_HIP(hipHostMalloc(&c->h_lres, sizeof(DevResults), hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_lres, sizeof(DevResults)));
     AQ_HIP(hipMalloc(&c->d_count, sizeof(unsigned) * (AQ_MAX_LEVELS + 2)));
-    int rc = reset_ctl(c);
-    if (rc) return rc;
     AQ_HIP(hipDeviceSynchronize());
     *out = c;
     return AQ_OK;
@@ -1212,6 +1226,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_x);
     (void)hipFree(c->d_y);
     if (c->h_slot) (void)hipHostFree(c->h_slot);
+    if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->h_lres) (void)hipHostFree(c->h_lres);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1268,7 +1283,7 @@ int aq_gather_results(aq_ctx* ctx, int first_slot, int n, void* d_out) {
     if (!ctx || !d_out || n < 0 || n > NSLOTS || first_slot < 0 || first_slot >= NSLOTS) return AQ_EINVAL;
     if (n == 0) return AQ_OK;
     AQ_HIP(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_out, first_slot, n, NSLOTS,
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_out, first_slot, n, NSLOTS,
                        (double*)d_out);
     AQ_HIP(hipGetLastError());
     return AQ_OK;

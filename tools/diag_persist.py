@@ -20,30 +20,23 @@ def summarize(d, f):
     t0 = col["t_start"].min()
     us = lambda v: (v - t0) / 100.0  # 100 MHz ticks -> us
     s = {}
-    for k in ("t_start", "t_seeded", "t_first_idle", "t_exit"):
+    for k in ("t_start", "t_seeded", "t_first_lead", "t_last_round", "t_exit"):
         v = us(col[k])
-        s[k] = {"min": v.min(), "p50": float(np.median(v)), "max": v.max()}
-    s["rounds"] = {"min": col["rounds"].min(), "p50": float(np.median(col["rounds"])), "max": col["rounds"].max()}
+        s[k] = {"min": round(v.min(), 2), "p50": round(float(np.median(v)), 2), "max": round(v.max(), 2)}
+    r = np.maximum(col["rounds"], 1)
+    s["rounds_per_wg"] = {"min": col["rounds"].min(), "p50": float(np.median(col["rounds"])), "max": col["rounds"].max()}
     s["lanes_per_round"] = float(col["active_lanes"].sum() / max(col["rounds"].sum(), 1))
-    busy = (col["t_first_idle"] - col["t_seeded"]) / 100.0
-    s["us_per_round_first_busy"] = float(np.median(busy / np.maximum(col["rounds"], 1)))
+    s["cyc_per_round"] = float(np.median(col["c_round"] / r))
+    s["cyc_eval_per_round"] = float(np.median(col["c_eval"] / r))
+    s["cyc_seed_p50"] = float(np.median(col["c_seed"]))
     s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
                   "sum": col["tasks"].sum()}
-    s["pool_push_w0"] = float(np.median(col["pool_push"]))
-    s["pool_take_w0"] = float(np.median(col["pool_take"]))
-    s["lock_spins_w0_max"] = col["lock_spins"].max()
-    s["spill_records"] = col["spill_records"].sum()
+    for k in ("leads", "pool_push", "pool_take", "lock_spins", "spill_records", "chunks_out", "chunks_in",
+              "records_out", "records_in"):
+        s[k] = {"sum": col[k].sum(), "max": col[k].max()}
+    s["t_wait_us_p50"] = float(np.median(col["t_wait"])) / 100.0
     s["max_ring"] = col["max_ring"].max()
-    s["chunks_out"] = col["chunks_out"].sum()
-    s["chunks_in"] = col["chunks_in"].sum()
-    s["records_moved"] = col["records_out"].sum()
-    s["t_produce_us_total"] = col["t_produce"].sum() / 100.0
-    s["t_idle_us_p50"] = float(np.median(col["t_idle"])) / 100.0
     s["seeds"] = {"min": col["seeds"].min(), "max": col["seeds"].max()}
-    r = np.maximum(col["rounds"], 1)
-    for k in ("c_round", "c_eval"):
-        s["cyc_per_round_" + k[2:]] = float(np.median(col[k] / r))
-    s["cyc_seed_p50"] = float(np.median(col["c_seed"]))
     return s
 
 
