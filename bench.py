@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-launch", type=int, default=256,
+                    help="integrals per persistent launch (1 = one launch per integral)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,6 +104,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.eps)
 
+    import numpy as np
     import torch
     import torch.distributed as dist
     from ppls_amd import Context, Problem
@@ -118,16 +121,27 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def run_steps(k, first_slot=0):
-        for i in range(k):
-            ctx.integrate_async(problem, (first_slot + i) % nslots, rank, world)
+    kmax = min(ctx.max_integrals_per_launch, nslots, args.per_launch)
+
+    def launch(m):
+        # m integrals of the workload in one persistent launch (slots 0..m-1), this rank's shard
+        ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank, nshards=world)
+
+    # single-integral latency (one integral per launch), reported beside the throughput
+    ctx.kernel_timing(True)
+    for _ in range(max(args.warmup, 5)):
+        launch(1)
+    ctx.synchronize()
+    single_ms, single_n = ctx.kernel_time()
+    ctx.kernel_timing(False)
 
     # warmup (also validates)
-    run_steps(args.warmup)
+    for _ in range(max(1, args.warmup // kmax)):
+        launch(kmax)
     ctx.synchronize()
 
     K = args.steps
-    buf = torch.zeros((min(K, nslots), 4), dtype=torch.float64, device="cuda")
+    buf = torch.zeros((kmax, 4), dtype=torch.float64, device="cuda")
     totals = torch.zeros((K, 4), dtype=torch.float64, device="cuda")
     ctx.kernel_timing(True)
     barrier()
@@ -135,8 +149,8 @@ def main():
     t0 = time.perf_counter()
     done = 0
     while done < K:
-        m = min(K - done, nslots)
-        run_steps(m, 0)
+        m = min(K - done, kmax)
+        launch(m)
         ctx.gather_results(0, m, buf.data_ptr())
         ctx.synchronize()
         chunk = buf[:m]
@@ -157,6 +171,7 @@ def main():
         elapsed, kern_avg_ms = float(tt[0]), float(tt[1])
     else:
         kern_avg_ms = kern_ms / max(launches, 1)
+    per_launch = K / max(launches, 1)
 
     # verify every timed step against the golden tree
     tot = totals.cpu().numpy()
@@ -169,8 +184,9 @@ def main():
     f_evals = tasks_total + 2 * K   # algorithmic F evaluations: 1 per task + F(A), F(B) per integral
 
     # this rank's share of the tasks per launch, for the roofline of its kernel
-    mine = ctx.fetch((K - 1) % nslots)
-    achieved = FLOP_PER_TASK * mine.tasks / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
+    mine = ctx.fetch(0)
+    tasks_per_launch = mine.tasks * per_launch
+    achieved = FLOP_PER_TASK * tasks_per_launch / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
 
     if rank == 0:
         out = {
@@ -191,12 +207,14 @@ def main():
                        "integrand": "cosh(x)^4 (aquadPartA.c:46)", "a": 0.0, "b": 5.0, "eps": args.eps,
                        "tasks_per_integral": int(tot[0, 1]), "accepted_per_integral": int(tot[0, 2]),
                        "parallelism": f"shard{world}" if world > 1 else "single-gpu",
+                       "integrals_per_launch": per_launch,
                        "workgroups_per_gpu": ctx.num_cus},
+            "single_integral_kernel_us": single_ms * 1e3 / max(single_n, 1),
             "verified": ok,
             "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(),
-                         "kernel": "aq::k_persist<0,false>", "kernel_avg_us": kern_avg_ms * 1e3,
-                         "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": mine.tasks},
+                         "kernel": "aq::k_stream<0,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
+                         "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": tasks_per_launch},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

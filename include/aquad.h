@@ -90,6 +90,13 @@ int aq_integrate_shard(aq_ctx *ctx, const aq_problem *p, int shard, int nshards,
  * results land in device slot `slot` (0 <= slot < aq_async_slots()); aq_fetch blocks for it. */
 int aq_async_slots(void);
 int aq_integrate_async(aq_ctx *ctx, const aq_problem *p, int shard, int nshards, int slot);
+/* K integrals of one integrand / eps / max_depth in ONE persistent launch (K <=
+ * aq_max_integrals_per_launch()): integral i has bounds [a[i], b[i]] and lands in slot first_slot+i
+ * (first_slot + k <= aq_async_slots()). The integrals share the machine: a wave that runs out of
+ * work on one integral seeds its share of the next, so the tail of each overlaps the next. */
+int aq_max_integrals_per_launch(void);
+int aq_integrate_many_async(aq_ctx *ctx, int integrand, int k, const double *a, const double *b, double eps,
+                            int max_depth, int shard, int nshards, int first_slot);
 int aq_fetch(aq_ctx *ctx, int slot, aq_result *res);
 int aq_synchronize(aq_ctx *ctx);
 /* Enqueue (on the context's stream) a copy of n consecutive slots' totals, starting at first_slot
@@ -123,7 +130,7 @@ int aq_eval_cosh(aq_ctx *ctx, size_t n, const double *x, double *out);
  * stream; aq_kernel_time returns the summed milliseconds and launch count since the last reset. */
 int aq_kernel_timing(aq_ctx *ctx, int enable);
 int aq_kernel_time(aq_ctx *ctx, double *total_ms, uint64_t *launches);
-/* Per-workgroup timeline of the persistent kernel (24 uint64 words per workgroup: realtime stamps
+/* Per-workgroup timeline of the persistent kernel (32 uint64 words per workgroup: realtime stamps
  * at entry / seeded / first idle / exit in 100 MHz ticks, rounds, tasks, chunks and records moved
  * through the HBM queue, produce/idle ticks, seeds, max stack depth, CU slot, records received,
  * active lanes summed over rounds, then shader-clock cycles per round phase and for seeding).

@@ -14,6 +14,7 @@ EXPORTS = (
     "aq_device_count", "aq_ctx_create", "aq_ctx_destroy", "aq_strerror", "aq_ctx_num_cus",
     "aq_set_level_histograms",
     "aq_integrate", "aq_integrate_shard", "aq_async_slots", "aq_integrate_async", "aq_fetch",
+    "aq_max_integrals_per_launch", "aq_integrate_many_async",
     "aq_synchronize", "aq_gather_results", "aq_integrate_levels", "aq_level_histogram", "aq_tasks_per_cu",
     "aq_integrate_batch", "aq_eval_integrand", "aq_eval_cosh", "aq_kernel_timing", "aq_kernel_time",
     "aq_set_diagnostics", "aq_diagnostics",
@@ -63,6 +64,9 @@ def load(build_if_missing=True):
         "aq_async_slots": ([], ctypes.c_int),
         "aq_integrate_async": ([vp, P, ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "aq_fetch": ([vp, ctypes.c_int, R], ctypes.c_int),
+        "aq_max_integrals_per_launch": ([], ctypes.c_int),
+        "aq_integrate_many_async": ([vp, ctypes.c_int, ctypes.c_int, dp, dp, ctypes.c_double, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "aq_synchronize": ([vp], ctypes.c_int),
         "aq_gather_results": ([vp, ctypes.c_int, ctypes.c_int, vp], ctypes.c_int),
         "aq_integrate_levels": ([vp, P, R, up, up, ctypes.c_int], ctypes.c_int),

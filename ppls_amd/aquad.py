@@ -153,6 +153,17 @@ class Context:
         _check(self.L.aq_integrate_async(self._h, ctypes.byref(problem.c()), shard, nshards, slot),
                "aq_integrate_async")
 
+    @property
+    def max_integrals_per_launch(self) -> int:
+        return self.L.aq_max_integrals_per_launch()
+
+    def integrate_many_async(self, a, b, eps, first_slot=0, integrand=COSH4, max_depth=0, shard=0, nshards=1):
+        """Enqueue len(a) integrals in one persistent launch; integral i lands in slot first_slot+i."""
+        a = np.ascontiguousarray(a, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        _check(self.L.aq_integrate_many_async(self._h, integrand, a.size, _dp(a), _dp(b), float(eps), max_depth,
+                                              shard, nshards, first_slot), "aq_integrate_many_async")
+
     def fetch(self, slot: int, detail=False) -> Result:
         r = _lib.aq_result()
         _check(self.L.aq_fetch(self._h, slot, ctypes.byref(r)), "aq_fetch")
@@ -176,8 +187,9 @@ class Context:
 
     DIAG_FIELDS = ("t_start", "t_seeded", "t_first_lead", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
                    "records_out", "t_wait", "leads", "seeds", "pool_push", "cu", "records_in", "active_lanes",
-                   "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed")
-    DIAG_WORDS = 24
+                   "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed",
+                   "c_seed1", "c_seed2", "c_seed3", "c_idle", "c_lock", "c_share", "give", "pad")
+    DIAG_WORDS = 32
 
     def set_diagnostics(self, enable: bool):
         _check(self.L.aq_set_diagnostics(self._h, 1 if enable else 0), "aq_set_diagnostics")

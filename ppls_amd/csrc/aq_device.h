@@ -1,0 +1,106 @@
+// aq_device.h -- device building blocks shared by the quadrature kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "aquad.h"
+#include "aq_libm.h"
+
+#pragma clang fp contract(off)
+
+namespace aq {
+
+enum : unsigned { ERRB_TIMEOUT = 1, ERRB_OVERFLOW = 2, ERRB_DEPTH = 4 };
+
+// Hardware CU slot of the executing wave: xcc*256 + (se*2 + sh)*16 + cu (HW_ID / XCC_ID registers).
+__device__ __forceinline__ unsigned cu_slot() {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, 32 bits
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID, bits 3:0
+    const unsigned cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
+    return ((xcc & 7u) << 8) | (((se << 1) | sh) << 4) | cu;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned wave_max_u(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ unsigned wave_or_u(unsigned v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= (unsigned)__shfl_xor((int)v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+__device__ __forceinline__ unsigned mbcnt(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// One trapezoid step of the reference (aquadPartA.c:185-191) on a record that carries F(l), F(r).
+// The operand order and association are the reference's; '/2' is exact (scaling by 2^-1).
+struct Step {
+    double mid, fmid, larea, rarea;
+    bool refine;
+};
+template <int FID>
+__device__ __forceinline__ Step task_step(double l, double r, double fl, double fr, double eps,
+                                          const ExpEntry* __restrict__ tab) {
+    Step s;
+    const double lrarea = (fl + fr) * (r - l) / 2;   // :185
+    s.mid = (l + r) / 2;                             // :187
+    s.fmid = integrand<FID>(s.mid, tab);             // :188
+    s.larea = (fl + s.fmid) * (s.mid - l) / 2;       // :189
+    s.rarea = (s.fmid + fr) * (r - s.mid) / 2;       // :190
+    s.refine = fabs((s.larea + s.rarea) - lrarea) > eps;  // :191 (strict >)
+    return s;
+}
+
+__device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ unsigned long long clk() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    return t;
+}
+
+// Write-through (sc1) global accesses for cross-CU hand-offs: the producer stores every payload
+// byte sc1 and drains vmcnt before one lane's sc1 flag store; the consumer polls the flag and
+// reads the payload with sc1 loads only (MI355X_MICROARCH.md, "Valid forms", row 1) -- no
+// release / acquire fences, whose L2 write-back / invalidate cost microseconds.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ unsigned ld_wt(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_add(int* p, int v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned g_add(unsigned* p, unsigned v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned g_ld(unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int g_ld(int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace aq

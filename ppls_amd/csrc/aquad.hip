@@ -33,6 +33,8 @@
 #include "aquad.h"
 #include "aq_exp_table.h"
 #include "aq_libm.h"
+#include "aq_device.h"
+#include "aq_stream.h"
 
 #pragma clang fp contract(off)
 
@@ -57,85 +59,6 @@ struct DevResults {
     unsigned long long cu_tasks[AQ_CU_SLOTS];
 };
 
-enum : unsigned { ERRB_TIMEOUT = 1, ERRB_OVERFLOW = 2, ERRB_DEPTH = 4 };
-
-// Persistent-path control block, one per async slot. It must be all-zero when a launch starts;
-// the host zeroes slots lazily in batches (one memset per 64 launches in sequential use) so a
-// launch needs no memset of its own. q_tokens stores (tokens - G): the HBM-queue protocol's
-// token count starts at G (every workgroup busy) and the run is over when it reaches 0.
-struct alignas(128) Line { unsigned v; unsigned pad[31]; };
-struct Ctl {
-    Line q_tail;               // chunk slots claimed by producers
-    Line q_head;               // tickets taken by idle workgroups
-    Line q_tokens;             // tokens - G
-    Line spare;
-    unsigned long long hist[2 * AQ_MAX_LEVELS];   // [0,L): tasks per level, [L,2L): accepted per level
-};
-
-constexpr int MAXG = 2048;     // max persistent workgroups per launch
-struct WgPart {                // one workgroup's share of a launch, plain stores at exit
-    double area;
-    unsigned long long tasks;
-    unsigned long long leaves;
-    unsigned long long spilled;
-    unsigned levels;
-    unsigned error;
-    unsigned cu;               // hardware CU slot
-    unsigned pad;
-};
-struct SlotOut {               // fully rewritten by every launch that targets the slot
-    unsigned nwg;
-    unsigned epoch;
-    unsigned pad[2];
-    WgPart wg[MAXG];
-};
-
-// Hardware CU slot of the executing wave: xcc*256 + (se*2 + sh)*16 + cu (HW_ID / XCC_ID registers).
-__device__ __forceinline__ unsigned cu_slot() {
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, 32 bits
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID, bits 3:0
-    const unsigned cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
-    return ((xcc & 7u) << 8) | (((se << 1) | sh) << 4) | cu;
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ unsigned wave_max_u(unsigned v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
-__device__ __forceinline__ unsigned mbcnt(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-
-// One trapezoid step of the reference (aquadPartA.c:185-191) on a record that carries F(l), F(r).
-// The operand order and association are the reference's; '/2' is exact (scaling by 2^-1).
-struct Step {
-    double mid, fmid, larea, rarea;
-    bool refine;
-};
-template <int FID>
-__device__ __forceinline__ Step task_step(double l, double r, double fl, double fr, double eps,
-                                          const ExpEntry* __restrict__ tab) {
-    Step s;
-    const double lrarea = (fl + fr) * (r - l) / 2;   // :185
-    s.mid = (l + r) / 2;                             // :187
-    s.fmid = integrand<FID>(s.mid, tab);             // :188
-    s.larea = (fl + s.fmid) * (s.mid - l) / 2;       // :189
-    s.rarea = (s.fmid + fr) * (r - s.mid) / 2;       // :190
-    s.refine = fabs((s.larea + s.rarea) - lrarea) > eps;  // :191 (strict >)
-    return s;
-}
 
 // ------------------------------------------------------------------------------------------------
 // Parity helper: evaluate F or cosh on an array.
@@ -253,675 +176,23 @@ __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsig
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Persistent on-device farmer.
-//
-// Work unit = an interval record {l, r, F(l), F(r), depth}. Worker = a WAVEFRONT: each of the NW
-// waves of a workgroup owns a ring of WCAP records in LDS and runs rounds of "pop <= 64 records,
-// evaluate F(mid) for each (aquadPartA.c:183-191), push the children (:192-197) with a ballot /
-// mbcnt compaction" with no workgroup barrier at all. Waves share work through a locked LDS pool
-// (overflow in, idle waves out); workgroups share work through an HBM ticket queue driven by one
-// elected leader wave per workgroup.
-// ------------------------------------------------------------------------------------------------
-constexpr int PT = 512;             // threads per workgroup
-constexpr int NW = PT / 64;         // waves (workers) per workgroup: 8, two per SIMD
-constexpr int WCAP = 256;           // per-wave LDS ring, records (power of two)
-constexpr int PCAP = 2048;          // per-workgroup LDS pool ring, records (power of two)
-constexpr int LREC = NW * WCAP + PCAP;   // LDS record slots: 4096 x 33 B = 132 KiB
-constexpr int POOL0 = NW * WCAP;    // first pool slot
-constexpr int CH = 512;             // records per HBM queue chunk
-constexpr int S_POS = 5;            // 2^S_POS seed positions per virtual worker (32..63 dealt)
-constexpr int GIVE_MIN = 96;        // a busy wave feeds the pool for idle siblings only above this depth
-constexpr int DONATE_MIN = 128;     // records needed before a workgroup donates to another CU
-constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
-
-// Write-through (sc1) global accesses for the chunk hand-off: the producer stores every payload
-// byte sc1 and drains vmcnt before one lane's sc1 flag store; the consumer polls the flag and
-// reads the payload with sc1 loads only (MI355X_MICROARCH.md, "Valid forms", row 1) -- no
-// release / acquire fences, whose L2 write-back / invalidate cost microseconds.
-__device__ __forceinline__ void st_wt(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_wt(unsigned* p, unsigned v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_wt(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(
-        reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ unsigned ld_wt(const unsigned* p) {
-    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int g_add(int* p, int v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned g_add(unsigned* p, unsigned v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned g_ld(unsigned* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
-// realtime stamps are s_memrealtime ticks (100 MHz), cycle counts are s_memtime shader cycles.
-enum : int {
-    DG_T_START = 0, DG_T_SEEDED, DG_T_FIRST_LEAD, DG_T_EXIT, DG_ROUNDS, DG_TASKS, DG_CHUNKS_OUT, DG_CHUNKS_IN,
-    DG_RECORDS_OUT, DG_T_WAIT, DG_LEADS, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
-    DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
-    DIAG_WORDS = 24
-};
-
-__device__ __forceinline__ unsigned long long clk() {
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    return t;
-}
-
-struct Chunk {                      // SoA, one queue slot
-    double l[CH], r[CH], fl[CH], fr[CH];
-    unsigned d[CH];
-    unsigned count;
-    unsigned pad[31];
-};
-
-struct PersistParams {
-    double a, b, eps, pad0;
-    int max_depth;
-    int shard, nshards;
-    int D;                          // seed depth
-    unsigned epoch;                 // tags queue slots of this call (ready[s] == epoch)
-    unsigned qcap;                  // queue slots
-    unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-    Ctl* ctl;
-    SlotOut* out;
-    unsigned long long* diag;          // optional per-workgroup timeline (DIAG_WORDS each), or null
-    Chunk* chunks;
-    unsigned* ready;
-    const ExpEntry* gtab;
-};
-
-__device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
-
-// Shared (LDS) state of one workgroup.
-struct WgState {
-    int lock;            // pool lock (lane 0 of the holding wave)
-    unsigned pbot, ptop; // pool ring, monotonic indices
-    int idle;            // waves with no records that are counted idle
-    int phase;           // 0 running, 1 a leader wave is at the HBM queue, 2 exit
-    int busy_token;      // the workgroup holds one token of the HBM-queue protocol
-    int err;
-    int pad;
-    unsigned top0[NW];   // seeded ring tops
-};
-
-// LDS record arrays (SoA), one per field.
-struct LdsRecs {
-    double* l;
-    double* r;
-    double* fl;
-    double* fr;
-    unsigned char* d;
-};
-
-__device__ __forceinline__ void wave_lock(int* lock, unsigned lane, unsigned long long& spins) {
-    if (lane == 0) {
-        int expect = 0;
-        while (!__hip_atomic_compare_exchange_strong(lock, &expect, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            expect = 0;
-            ++spins;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__device__ __forceinline__ void wave_unlock(int* lock, unsigned lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) __hip_atomic_store(lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Copy one record (LDS slot i -> LDS slot j).
-__device__ __forceinline__ void copy_rec(const LdsRecs& R, unsigned i, unsigned j) {
-    const double l = R.l[i], r = R.r[i], fl = R.fl[i], fr = R.fr[i];
-    const unsigned char d = R.d[i];
-    R.l[j] = l; R.r[j] = r; R.fl[j] = fl; R.fr[j] = fr; R.d[j] = d;
-}
-
-// Publish k records (LDS slots src(i), i < k, i.e. base..) as HBM chunk `slot` (caller: one whole wave).
-template <typename SrcIdx>
-__device__ __forceinline__ void publish_chunk(const PersistParams& P, const LdsRecs& R, unsigned slot, unsigned k,
-                                              SrcIdx src, unsigned lane) {
-    Chunk* __restrict__ c = P.chunks + slot;
-    for (unsigned i = lane; i < k; i += 64) {
-        const unsigned j = src(i);
-        st_wt(&c->l[i], R.l[j]); st_wt(&c->r[i], R.r[j]); st_wt(&c->fl[i], R.fl[j]);
-        st_wt(&c->fr[i], R.fr[j]); st_wt(&c->d[i], (unsigned)R.d[j]);
-    }
-    if (lane == 0) st_wt(&c->count, k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the single storing wave drains
-    if (lane == 0) st_wt(&P.ready[slot], P.epoch);
-}
-
-template <int FID, bool HIST, bool DIAG>
-__global__ __launch_bounds__(PT) void k_persist(PersistParams P) {
-    __shared__ double s_l[LREC], s_r[LREC], s_fl[LREC], s_fr[LREC];
-    __shared__ unsigned char s_d[LREC];
-    __shared__ ExpEntry tab[128];
-    __shared__ WgState S;
-    __shared__ double s_red[NW];
-    __shared__ unsigned s_redu[3][NW];
-    __shared__ unsigned long long s_spill[NW];
-    __shared__ unsigned s_hist[HIST ? 2 * AQ_MAX_LEVELS : 1];
-
-    const unsigned tid = threadIdx.x;
-    const unsigned lane = lane_id();
-    const unsigned wid = tid >> 6;
-    Ctl* __restrict__ ctl = P.ctl;
-    const LdsRecs R{s_l, s_r, s_fl, s_fr, s_d};
-    const unsigned long long t_entry = rtc();
-    const unsigned long long c_entry = DIAG ? clk() : 0ull;
-    __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];  // diagnostics (DIAG builds only)
-    if (DIAG) {
-        for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
-    }
-    stage_exp_table(tab, P.gtab);
-    if (HIST)
-        for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) s_hist[i] = 0;
-    if (tid == 0) {
-        S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1; S.err = 0;
-    }
-
-    const double eps = P.eps;
-    const int max_depth = P.max_depth;
-    double my_area = 0.0;
-    unsigned my_tasks = 0, my_leaves = 0, my_maxd = 0;
-    unsigned err = 0;
-
-    // ---------------- seeding: this worker's depth-D positions, all F evaluations in one pass ----
-    // Virtual worker vwg of V owns positions j = k*V + (k odd ? V-1-vwg : vwg) < 2^D (snake order
-    // over bands). Every ancestor of every position is a task; its decision is the reference's
-    // arithmetic on (l, r, F(l), F(r), F(mid)), all of which are F at mids of the position's own
-    // path or at A/B. A task above depth D is counted by the owner of its leftmost descendant.
-    const unsigned V = gridDim.x * (unsigned)P.nshards;
-    const unsigned vwg = blockIdx.x * (unsigned)P.nshards + (unsigned)P.shard;
-    const int D = P.D;
-    const unsigned long long npos_total = 1ull << D;
-    const unsigned nb = (unsigned)((npos_total + V - 1) / V);  // bands = positions per worker (<= 64)
-    const unsigned npairs = (unsigned)D * nb;
-    auto position = [&](unsigned k, bool& valid) -> unsigned long long {
-        const unsigned long long o = (k & 1u) ? (unsigned long long)(V - 1 - vwg) : (unsigned long long)vwg;
-        const unsigned long long j = (unsigned long long)k * V + o;
-        valid = j < npos_total;
-        return j;
-    };
-    // scratch in the (still empty) pool region
-    double* fm = s_l + POOL0;          // [npairs + 2]: F(mid of node (d,k)) at d*nb+k, then F(A), F(B)
-    double* leafa = s_r + POOL0;       // [npairs]: larea + rarea of node (d,k)
-    unsigned char* flag = s_d + POOL0; // [npairs]: node (d,k) refines
-    for (unsigned q = tid; q < npairs + 2; q += PT) {
-        double x;
-        if (q < npairs) {
-            const unsigned d = q / nb, k = q % nb;
-            bool valid;
-            const unsigned long long p = position(k, valid);
-            const unsigned long long anc = valid ? (p >> (D - (int)d)) : 0ull;
-            double l = P.a, r = P.b;
-            for (unsigned i = 0; i < d; ++i) {
-                const double m = (l + r) / 2;
-                if ((anc >> (d - 1 - i)) & 1ull) l = m; else r = m;
-            }
-            x = (l + r) / 2;
-        } else {
-            x = (q == npairs) ? P.a : P.b;
-        }
-        fm[q] = x;
-    }
-    __syncthreads();  // exp table staged
-    for (unsigned q = tid; q < npairs + 2; q += PT) fm[q] = integrand<FID>(fm[q], tab);
-    __syncthreads();
-    for (unsigned q = tid; q < npairs; q += PT) {
-        const unsigned d = q / nb, k = q % nb;
-        bool valid;
-        const unsigned long long p = position(k, valid);
-        const unsigned long long anc = valid ? (p >> (D - (int)d)) : 0ull;
-        double l = P.a, r = P.b;
-        unsigned li = npairs, ri = npairs + 1;
-        for (unsigned i = 0; i < d; ++i) {
-            const double m = (l + r) / 2;
-            if ((anc >> (d - 1 - i)) & 1ull) { l = m; li = i * nb + k; } else { r = m; ri = i * nb + k; }
-        }
-        const double fl = fm[li], fr = fm[ri], fmid = fm[q];
-        const double mid = (l + r) / 2;
-        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
-        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
-        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
-        flag[q] = fabs((larea + rarea) - lrarea) > eps;      // :191
-        leafa[q] = larea + rarea;                             // :199
-    }
-    __syncthreads();
-    if (wid == 0) {
-        const unsigned k = lane;
-        bool valid = false;
-        const unsigned long long p = (k < nb) ? position(k, valid) : 0ull;
-        // every flag of this position's path in one batch of independent LDS reads
-        unsigned long long fmask = 0;
-        for (int d = 0; d < D; ++d)
-            fmask |= (unsigned long long)(flag[(unsigned)d * nb + (k < nb ? k : 0)] ? 1u : 0u) << d;
-        const int dstar = (int)__builtin_ctzll(~fmask);   // first depth that does not refine (D if none)
-        bool alive = valid;
-        if (valid) {
-            const int dlast = min(dstar, D - 1);
-            for (int d = 0; d <= dlast; ++d) {
-                const bool owner = (p & ((1ull << (D - d)) - 1ull)) == 0ull;
-                if (owner) {
-                    ++my_tasks;
-                    my_maxd = max(my_maxd, (unsigned)d + 1u);
-                    if (HIST) atomicAdd(&s_hist[d], 1u);
-                    if (d == dstar) {
-                        my_area += leafa[(unsigned)d * nb + k];
-                        ++my_leaves;
-                        if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
-                    } else if (d + 1 >= max_depth) {
-                        err |= ERRB_DEPTH;
-                    }
-                }
-            }
-            alive = dstar >= D && D < max_depth;
-        }
-        double l = P.a, r = P.b, fl = 0.0, fr = 0.0;
-        if (alive) {
-            unsigned li = npairs, ri = npairs + 1;
-            for (int i = 0; i < D; ++i) {
-                const double m = (l + r) / 2;
-                if ((p >> (D - 1 - i)) & 1ull) { l = m; li = (unsigned)i * nb + k; } else { r = m; ri = (unsigned)i * nb + k; }
-            }
-            fl = fm[li];
-            fr = fm[ri];
-        }
-        // seed k goes to wave k % NW
-        for (unsigned w = 0; w < NW; ++w) {
-            const unsigned long long m = __ballot(alive && (k % NW) == w);
-            if (alive && (k % NW) == w) {
-                const unsigned j = w * WCAP + mbcnt(m);
-                s_l[j] = l; s_r[j] = r; s_fl[j] = fl; s_fr[j] = fr; s_d[j] = (unsigned char)D;
-            }
-            if (lane == 0) S.top0[w] = (unsigned)__popcll(m);
-        }
-    }
-    __syncthreads();
-
-    // ---------------- main loop: every wave is an independent worker ----------------
-    const unsigned base = wid * WCAP;            // this wave's ring
-    unsigned top = S.top0[wid], bot = 0;         // wave-uniform
-    if constexpr (DIAG) {
-        if (tid == 0) {
-            s_dg[DG_T_START] = t_entry;
-            s_dg[DG_T_SEEDED] = rtc();
-            s_dg[DG_C_SEED] = clk() - c_entry;
-            unsigned n = 0;
-            for (int w = 0; w < NW; ++w) n += S.top0[w];
-            s_dg[DG_SEEDS] = n;
-        }
-    }
-    const unsigned long long t0 = rtc();
-    bool counted_idle = false;                    // wave-uniform
-    unsigned poll_ctr = wid * (POLL_ROUNDS / NW);
-    unsigned seen_head = 0, seen_tail = 0;        // lane 0's view of the HBM queue
-    unsigned long long spilled = 0;               // records this wave sent to HBM (lane 0)
-    unsigned long long lock_spins = 0;
-
-    for (;;) {
-        unsigned size = top - bot;
-
-        if (size == 0) {
-            // ---- out of records: take from the pool, else idle / lead the workgroup to the HBM queue
-            if (counted_idle) {
-                // already counted idle: peek without the lock (the wave whose increment made every
-                // wave idle is the one that leads, so a counted wave only waits here)
-                const unsigned pt = __hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const unsigned pb = __hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int ph = __hip_atomic_load(&S.phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (pt == pb) {
-                    if (ph == 2) break;
-                    __builtin_amdgcn_s_sleep(4);
-                    continue;
-                }
-            }
-            wave_lock(&S.lock, lane, lock_spins);
-            const unsigned avail = S.ptop - S.pbot;
-            const int phase = S.phase;
-            unsigned k = 0;
-            bool lead = false;
-            if (avail > 0) {
-                k = min(avail, 64u);
-                const unsigned pb = S.pbot;
-                if (lane < k) copy_rec(R, POOL0 + ((pb + lane) & (PCAP - 1)), base + lane);
-                if (lane == 0) {
-                    S.pbot = pb + k;
-                    if (counted_idle) S.idle -= 1;
-                }
-                counted_idle = false;
-            } else {
-                if (!counted_idle) {
-                    if (lane == 0) S.idle += 1;
-                    counted_idle = true;
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (phase == 0 && S.idle == NW) {   // every wave idle and the pool empty
-                    lead = true;
-                    if (lane == 0) S.phase = 1;
-                }
-            }
-            wave_unlock(&S.lock, lane);
-            if constexpr (DIAG) { if (lane == 0 && k) atomicAdd(&s_dg[DG_POOL_TAKE], (unsigned long long)k); }
-            if (k) {
-                bot = 0;
-                top = k;
-                continue;
-            }
-            if (phase == 2) break;
-            if (!lead) {
-                __builtin_amdgcn_s_sleep(4);
-                continue;
-            }
-            // ---- leader: this workgroup has no work; hand its token back and wait for a chunk
-            unsigned long long tl = DIAG ? rtc() : 0ull;
-            if constexpr (DIAG) {
-                if (lane == 0) {
-                    atomicMin(&s_dg[DG_T_FIRST_LEAD], tl);
-                    atomicAdd(&s_dg[DG_LEADS], 1ull);
-                }
-            }
-            int cmd = -1;   // >= 0 chunk slot, -1 exit, -2 error
-            unsigned cnt = 0;
-            if (lane == 0) {
-                if (S.busy_token) {
-                    g_add((int*)&ctl->q_tokens.v, -1);
-                    S.busy_token = 0;
-                }
-                const unsigned h = g_add(&ctl->q_head.v, 1u);
-                for (unsigned spins = 0;; ++spins) {
-                    if (h < P.qcap && ld_wt(&P.ready[h]) == P.epoch) { cmd = (int)h; break; }
-                    if ((spins & 3u) == 0u &&
-                            __hip_atomic_load((int*)&ctl->q_tokens.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                            -(int)gridDim.x) {
-                        cmd = -1;
-                        break;
-                    }
-                    if ((spins & 63u) == 63u && rtc() - t0 > P.timeout_ticks) { err |= ERRB_TIMEOUT; cmd = -2; break; }
-                    __builtin_amdgcn_s_sleep(8);
-                }
-                if (cmd >= 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-                    cnt = ld_wt(&P.chunks[cmd].count);
-                }
-            }
-            cmd = __shfl(cmd, 0, 64);
-            cnt = __shfl(cnt, 0, 64);
-            if (cmd < 0) {
-                wave_lock(&S.lock, lane, lock_spins);
-                if (lane == 0) S.phase = 2;
-                wave_unlock(&S.lock, lane);
-                break;
-            }
-            // load the chunk into the (empty) pool, take this workgroup's token back
-            const Chunk* __restrict__ c = P.chunks + cmd;
-            wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = S.ptop;
-            for (unsigned i = lane; i < cnt; i += 64) {
-                const unsigned j = POOL0 + ((pt + i) & (PCAP - 1));
-                s_l[j] = ld_wt(&c->l[i]); s_r[j] = ld_wt(&c->r[i]); s_fl[j] = ld_wt(&c->fl[i]);
-                s_fr[j] = ld_wt(&c->fr[i]); s_d[j] = (unsigned char)ld_wt(&c->d[i]);
-            }
-            if (lane == 0) {
-                S.ptop = pt + cnt;
-                S.phase = 0;
-                S.busy_token = 1;
-                S.idle -= 1;   // the leader un-counts itself, so an empty chunk leads to a new leader
-                g_add((int*)&ctl->q_tokens.v, 1 - (int)cnt);
-            }
-            counted_idle = false;
-            wave_unlock(&S.lock, lane);
-            if constexpr (DIAG) {
-                if (lane == 0) {
-                    atomicAdd(&s_dg[DG_CHUNKS_IN], 1ull);
-                    atomicAdd(&s_dg[DG_RECORDS_IN], (unsigned long long)cnt);
-                    atomicAdd(&s_dg[DG_T_WAIT], rtc() - tl);
-                }
-            }
-            continue;
-        }
-
-        // ---- keep the ring from overflowing: move its bottom 64 records to the pool, else to HBM
-        if (size > (unsigned)(WCAP - 64)) {
-            wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = S.ptop;
-            const bool fits = (pt - S.pbot) + 64u <= (unsigned)PCAP;
-            if (fits) {
-                copy_rec(R, base + ((bot + lane) & (WCAP - 1)), POOL0 + ((pt + lane) & (PCAP - 1)));
-                if (lane == 0) S.ptop = pt + 64u;
-            }
-            wave_unlock(&S.lock, lane);
-            if (!fits) {
-                // pool full: spill 64 records to an HBM chunk (tokens first, then publish)
-                unsigned slot = 0;
-                if (lane == 0) {
-                    slot = g_add(&ctl->q_tail.v, 1u);
-                    if (slot < P.qcap) g_add((int*)&ctl->q_tokens.v, 64);
-                    spilled += 64;
-                }
-                slot = __shfl(slot, 0, 64);
-                if (slot < P.qcap) {
-                    const unsigned b = bot;
-                    publish_chunk(P, R, slot, 64u, [&](unsigned i) { return base + ((b + i) & (WCAP - 1)); }, lane);
-                } else {
-                    err |= ERRB_OVERFLOW;   // records dropped: result invalid, error reported
-                }
-            }
-            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_POOL_PUSH], 64ull); }
-            bot += 64;
-            continue;
-        }
-
-        // ---- feed idle sibling waves / donate to starving workgroups
-        if (size >= (unsigned)GIVE_MIN && S.idle > 0 && S.ptop == S.pbot) {
-            const unsigned k = size / 2u;   // <= 128
-            wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = S.ptop;
-            const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
-            if (fits) {
-                for (unsigned i = lane; i < k; i += 64)
-                    copy_rec(R, base + ((bot + i) & (WCAP - 1)), POOL0 + ((pt + i) & (PCAP - 1)));
-                if (lane == 0) S.ptop = pt + k;
-            }
-            wave_unlock(&S.lock, lane);
-            if (fits) {
-                bot += k;
-                continue;
-            }
-        }
-        if (((++poll_ctr) % POLL_ROUNDS) == 0) {
-            // another CU waits on the HBM queue and this workgroup has plenty: donate from the pool
-            // (its oldest, i.e. shallowest, records) or from the bottom of this ring
-            unsigned slot = 0xffffffffu;
-            if (lane == 0) {
-                if ((int)(seen_head - seen_tail) > 0) {
-                    unsigned expect = seen_tail;
-                    if (__hip_atomic_compare_exchange_strong(&ctl->q_tail.v, &expect, seen_tail + 1u, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                        slot = seen_tail;
-                }
-                seen_head = g_ld(&ctl->q_head.v);
-                seen_tail = g_ld(&ctl->q_tail.v);
-            }
-            slot = __shfl(slot, 0, 64);
-            if (slot != 0xffffffffu) {
-                if (slot >= P.qcap) {
-                    err |= ERRB_OVERFLOW;
-                } else {
-                    wave_lock(&S.lock, lane, lock_spins);
-                    const unsigned pavail = S.ptop - S.pbot;
-                    unsigned k;
-                    if (pavail >= (unsigned)DONATE_MIN) {
-                        k = min((unsigned)CH, pavail / 2u);
-                        const unsigned pb = S.pbot;
-                        if (lane == 0) g_add((int*)&ctl->q_tokens.v, (int)k);
-                        publish_chunk(P, R, slot, k, [&](unsigned i) { return POOL0 + ((pb + i) & (PCAP - 1)); }, lane);
-                        if (lane == 0) S.pbot = pb + k;
-                        wave_unlock(&S.lock, lane);
-                    } else {
-                        wave_unlock(&S.lock, lane);
-                        k = size / 2u;   // may be 0: an empty chunk is harmless
-                        if (lane == 0) g_add((int*)&ctl->q_tokens.v, (int)k);
-                        const unsigned b = bot;
-                        publish_chunk(P, R, slot, k, [&](unsigned i) { return base + ((b + i) & (WCAP - 1)); }, lane);
-                        bot += k;
-                    }
-                    if (lane == 0) spilled += k;
-                    if constexpr (DIAG) {
-                        if (lane == 0) {
-                            atomicAdd(&s_dg[DG_CHUNKS_OUT], 1ull);
-                            atomicAdd(&s_dg[DG_RECORDS_OUT], (unsigned long long)k);
-                        }
-                    }
-                    continue;
-                }
-            }
-        }
-
-        // ---- one round: pop up to 64 records from the top of this wave's ring
-        unsigned long long c0 = 0, c1 = 0;
-        if constexpr (DIAG) c0 = clk();
-        const unsigned n = min(size, 64u);
-        const unsigned b0 = top - n;
-        const bool active = lane < n;
-        double l = 0, r = 0, fl = 0, fr = 0;
-        unsigned d = 0;
-        if (active) {
-            const unsigned j = base + ((b0 + lane) & (WCAP - 1));
-            l = s_l[j]; r = s_r[j]; fl = s_fl[j]; fr = s_fr[j]; d = s_d[j];
-        }
-        bool refine = false;
-        double mid = 0, fmid = 0;
-        if (active) {
-            const Step st = task_step<FID>(l, r, fl, fr, eps, tab);
-            mid = st.mid;
-            fmid = st.fmid;
-            ++my_tasks;
-            my_maxd = max(my_maxd, d + 1u);
-            if (HIST) atomicAdd(&s_hist[d], 1u);
-            if (st.refine) {
-                if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
-                else refine = true;
-            } else {
-                my_area += st.larea + st.rarea;  // :199 -> :149
-                ++my_leaves;
-                if (HIST) atomicAdd(&s_hist[AQ_MAX_LEVELS + d], 1u);
-            }
-        }
-        if constexpr (DIAG) c1 = clk();
-        const unsigned long long mask = __ballot(refine);
-        if (refine) {
-            const unsigned pos = b0 + 2u * mbcnt(mask);
-            const unsigned j0 = base + (pos & (WCAP - 1)), j1 = base + ((pos + 1u) & (WCAP - 1));
-            const unsigned char cd = (unsigned char)(d + 1u);
-            s_l[j0] = l;   s_r[j0] = mid; s_fl[j0] = fl;   s_fr[j0] = fmid; s_d[j0] = cd;  // [l,mid]  :192-194
-            s_l[j1] = mid; s_r[j1] = r;   s_fl[j1] = fmid; s_fr[j1] = fr;   s_d[j1] = cd;  // [mid,r]  :195-197
-        }
-        top = b0 + 2u * (unsigned)__popcll(mask);
-        if constexpr (DIAG) {
-            if (lane == 0) {
-                const unsigned long long c2 = clk();
-                atomicAdd(&s_dg[DG_ROUNDS], 1ull);
-                atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
-                atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
-                atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
-                atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)size);
-                atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
-            }
-        }
-    }
-
-    // ---------------- exit: this workgroup's partial results, plain stores (no contention) ------
-    const double wa = wave_sum(my_area);
-    const unsigned wt = wave_sum_u(my_tasks), wl = wave_sum_u(my_leaves), wm = wave_max_u(my_maxd);
-    unsigned we = err;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) we |= (unsigned)__shfl_xor((int)we, o, 64);
-    if (lane == 0) {
-        s_red[wid] = wa;
-        s_redu[0][wid] = wt;
-        s_redu[1][wid] = wl;
-        s_redu[2][wid] = wm;
-        s_spill[wid] = spilled | ((unsigned long long)we << 48);
-        if constexpr (DIAG) {
-            atomicAdd(&s_dg[DG_LOCK_SPINS], lock_spins);
-            atomicAdd(&s_dg[DG_SPILL_RECORDS], spilled);
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        double ba = 0.0;
-        unsigned bt = 0, bl = 0, bm = 0, be = 0;
-        unsigned long long bs = 0;
-        for (int w = 0; w < NW; ++w) {
-            ba += s_red[w];
-            bt += s_redu[0][w];
-            bl += s_redu[1][w];
-            bm = max(bm, s_redu[2][w]);
-            bs += s_spill[w] & 0xffffffffffffull;
-            be |= (unsigned)(s_spill[w] >> 48);
-        }
-        WgPart* o = &P.out->wg[blockIdx.x];
-        o->area = ba;
-        o->tasks = bt;
-        o->leaves = bl;
-        o->spilled = bs;
-        o->levels = bm;
-        o->error = be;
-        o->cu = cu_slot();
-        if (blockIdx.x == 0) {
-            P.out->nwg = gridDim.x;
-            P.out->epoch = P.epoch;
-        }
-        if constexpr (DIAG) {
-            s_dg[DG_T_EXIT] = rtc();
-            s_dg[DG_CU] = cu_slot();
-            s_dg[DG_TASKS] = bt;
-            unsigned long long* d = P.diag + (size_t)blockIdx.x * DIAG_WORDS;
-            for (int i = 0; i < DIAG_WORDS; ++i) d[i] = s_dg[i];
-        }
-    }
-    if (HIST) {
-        for (unsigned i = tid; i < 2 * AQ_MAX_LEVELS; i += PT) {
-            const unsigned v = s_hist[i];
-            if (v) atomicAdd(&ctl->hist[i], (unsigned long long)v);
-        }
-    }
-}
-
 // Gather n slots' totals into a caller device buffer as f64 [area, tasks, accepted, error] rows,
 // ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot sums the
 // slot's per-workgroup partials in a fixed order.
-__global__ __launch_bounds__(256) void k_gather(const SlotOut* __restrict__ slots, int first, int n, int nslots,
+__global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts, int G, int first, int n, int nslots,
                                                 double* __restrict__ out) {
     __shared__ double s_a[4];
     __shared__ unsigned long long s_t[4], s_l[4];
     __shared__ unsigned s_e[4];
-    const SlotOut& s = slots[(first + (int)blockIdx.x) % nslots];
-    const unsigned nwg = min(s.nwg, (unsigned)MAXG);
+    const WgPart* w = parts + (size_t)((first + (int)blockIdx.x) % nslots) * G;
     double a = 0.0;
     unsigned long long t = 0, l = 0;
     unsigned e = 0;
-    for (unsigned i = threadIdx.x; i < nwg; i += blockDim.x) {
-        a += s.wg[i].area;
-        t += s.wg[i].tasks;
-        l += s.wg[i].leaves;
-        e |= s.wg[i].error;
+    for (int i = threadIdx.x; i < G; i += blockDim.x) {
+        a += w[i].area;
+        t += w[i].tasks;
+        l += w[i].leaves;
+        e |= w[i].error;
     }
     a = wave_sum(a);
 #pragma unroll
@@ -930,8 +201,8 @@ __global__ __launch_bounds__(256) void k_gather(const SlotOut* __restrict__ slot
         l += __shfl_xor(l, o, 64);
         e |= (unsigned)__shfl_xor((int)e, o, 64);
     }
-    const unsigned w = threadIdx.x >> 6;
-    if (lane_id() == 0) { s_a[w] = a; s_t[w] = t; s_l[w] = l; s_e[w] = e; }
+    const unsigned wv = threadIdx.x >> 6;
+    if (lane_id() == 0) { s_a[wv] = a; s_t[wv] = t; s_l[wv] = l; s_e[wv] = e; }
     __syncthreads();
     if (threadIdx.x == 0) {
         double A = 0.0;
@@ -957,6 +228,7 @@ namespace {
 
 constexpr int NSLOTS = 256;
 constexpr unsigned QCAP = 16384;  // HBM queue slots (16384 x 17 KiB = 273 MiB)
+static_assert(MAXK <= NSLOTS, "a launch's integrals need distinct slots");
 
 #define AQ_HIP(call)                                                                  \
     do {                                                                              \
@@ -975,22 +247,24 @@ int err_from_bits(unsigned bits) {
     return AQ_OK;
 }
 
-int ceil_log2(unsigned v) {
+int ceil_log2(unsigned long long v) {
     int d = 0;
-    while ((1u << d) < v) ++d;
+    while ((1ull << d) < v) ++d;
     return d;
 }
+
+bool bounds_ok(double a, double b) { return std::isfinite(a) && std::isfinite(b) && b >= a; }
 
 int validate(const aq_problem* p) {
     if (!p) return AQ_EINVAL;
     if (p->integrand != AQ_F_COSH4 && p->integrand != AQ_F_SIN_RECIP) return AQ_EINVAL;
-    if (!std::isfinite(p->a) || !std::isfinite(p->b) || !(p->b >= p->a)) return AQ_EINVAL;
+    if (!bounds_ok(p->a, p->b)) return AQ_EINVAL;
     if (!(p->eps >= 0.0)) return AQ_EINVAL;
     if (p->max_depth < 0 || p->max_depth > AQ_MAX_LEVELS - 1) return AQ_EINVAL;
     return AQ_OK;
 }
 
-// Host view of one finished call, whichever path produced it.
+// Host view of one finished integral, whichever path produced it.
 struct HostOut {
     double area = 0.0;
     unsigned long long tasks = 0, leaves = 0, spilled = 0;
@@ -1004,14 +278,16 @@ struct HostOut {
 struct aq_ctx {
     int device = 0;
     int num_cus = 0;
-    int persist_grid = 0;
+    int grid = 0;                      // persistent workgroups per launch (one per CU)
     bool histograms = true;
     hipStream_t stream = nullptr;
     ExpEntry* d_tab = nullptr;
-    Ctl* d_ctl = nullptr;              // NSLOTS control blocks
-    bool ctl_dirty[NSLOTS] = {};       // slot's control block used since it was last zeroed
-    SlotOut* d_out = nullptr;          // NSLOTS
+    Ctl* d_ctl = nullptr;              // NSLOTS control blocks (queue + per-integral histograms)
+    WgPart* d_parts = nullptr;         // NSLOTS x grid per-workgroup partials
+    bool dirty[NSLOTS] = {};           // slot's ctl / parts used since they were last zeroed
     bool slot_hist[NSLOTS] = {};
+    double2* d_bounds = nullptr;       // NSLOTS {a, b}
+    double2* h_bounds = nullptr;       // pinned staging, NSLOTS
     Chunk* d_chunks = nullptr;
     unsigned* d_ready = nullptr;
     unsigned epoch = 0;
@@ -1025,7 +301,7 @@ struct aq_ctx {
     double* d_y = nullptr;
     size_t eval_cap = 0;
     // host staging
-    SlotOut* h_slot = nullptr;         // pinned
+    WgPart* h_parts = nullptr;         // pinned, grid entries
     unsigned long long* h_hist = nullptr;  // pinned, 2 * AQ_MAX_LEVELS
     DevResults* h_lres = nullptr;      // pinned
     HostOut last;
@@ -1042,40 +318,49 @@ struct aq_ctx {
 
 namespace {
 
-// Zero the control block of `slot` (and of the following slots up to a batch of 64) if it has
-// been used since it was last zeroed: one memset per 64 launches when slots are used in order.
-int ensure_clean(aq_ctx* c, int slot) {
-    if (!c->ctl_dirty[slot]) return AQ_OK;
-    int n = 0;
-    while (slot + n < NSLOTS && n < 64) c->ctl_dirty[slot + n++] = false;
-    AQ_HIP(hipMemsetAsync(c->d_ctl + slot, 0, sizeof(Ctl) * (size_t)n, c->stream));
+// Zero the control blocks and partials of slots [s, s+k) if any was used since it was last zeroed;
+// the zeroed range is extended to a batch of 64 slots, so sequential use costs one memset pair per
+// 64 integrals and a launch needs no memset of its own.
+int ensure_clean(aq_ctx* c, int s, int k) {
+    bool need = false;
+    for (int i = s; i < s + k; ++i) need |= c->dirty[i];
+    if (!need) return AQ_OK;
+    const int e = std::min(NSLOTS, std::max(s + k, s + 64));
+    for (int i = s; i < e; ++i) c->dirty[i] = false;
+    AQ_HIP(hipMemsetAsync(c->d_ctl + s, 0, sizeof(Ctl) * (size_t)(e - s), c->stream));
+    AQ_HIP(hipMemsetAsync(c->d_parts + (size_t)s * c->grid, 0, sizeof(WgPart) * (size_t)(e - s) * c->grid,
+                          c->stream));
     return AQ_OK;
 }
 
 template <int FID, bool HIST>
-int launch_persist(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int slot) {
-    const int G = ctx->persist_grid;
-    PersistParams P{};
-    P.a = p->a;
-    P.b = p->b;
-    P.eps = p->eps;
-    P.max_depth = p->max_depth ? p->max_depth : AQ_DEFAULT_MAX_DEPTH;
+int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double eps, int max_depth, int shard,
+                  int nshards, int first_slot) {
+    const int G = ctx->grid;
+    int rc = ensure_clean(ctx, first_slot, k);
+    if (rc) return rc;
+    for (int i = 0; i < k; ++i) ctx->h_bounds[first_slot + i] = make_double2(a[i], b[i]);
+    AQ_HIP(hipMemcpyAsync(ctx->d_bounds + first_slot, ctx->h_bounds + first_slot, sizeof(double2) * (size_t)k,
+                          hipMemcpyHostToDevice, ctx->stream));
+    StreamParams P{};
+    P.bounds = ctx->d_bounds + first_slot;
+    P.nprob = k;
+    P.first_slot = first_slot;
+    P.eps = eps;
+    P.max_depth = max_depth ? max_depth : AQ_DEFAULT_MAX_DEPTH;
     P.shard = shard;
     P.nshards = nshards;
-    const unsigned V = (unsigned)G * (unsigned)nshards;
-    P.D = ceil_log2(V) + S_POS;
+    P.D = ceil_log2((unsigned long long)G * NW * (unsigned long long)nshards) + S_W;
     P.epoch = ++ctx->epoch;
     if (P.epoch == 0) P.epoch = ++ctx->epoch;
     P.qcap = QCAP;
     P.timeout_ticks = 100000000ull * 20ull;  // 20 s of the 100 MHz realtime clock
-    int rc = ensure_clean(ctx, slot);
-    if (rc) return rc;
-    P.ctl = ctx->d_ctl + slot;
-    P.out = ctx->d_out + slot;
+    P.ctls = ctx->d_ctl;
+    P.parts = ctx->d_parts;
+    P.diag = ctx->d_diag;
     P.chunks = ctx->d_chunks;
     P.ready = ctx->d_ready;
     P.gtab = ctx->d_tab;
-    P.diag = ctx->d_diag;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (ctx->timing) {
         if (!ctx->ev_free.empty()) {
@@ -1088,16 +373,18 @@ int launch_persist(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int
         AQ_HIP(hipEventRecord(ev.first, ctx->stream));
     }
     if (P.diag)
-        hipLaunchKernelGGL((k_persist<FID, HIST, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
+        hipLaunchKernelGGL((k_stream<FID, HIST, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
     else
-        hipLaunchKernelGGL((k_persist<FID, HIST, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
+        hipLaunchKernelGGL((k_stream<FID, HIST, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
     AQ_HIP(hipGetLastError());
     if (ctx->timing) {
         AQ_HIP(hipEventRecord(ev.second, ctx->stream));
         ctx->ev_pending.push_back(ev);
     }
-    ctx->slot_hist[slot] = HIST;
-    ctx->ctl_dirty[slot] = true;
+    for (int i = first_slot; i < first_slot + k; ++i) {
+        ctx->dirty[i] = true;
+        ctx->slot_hist[i] = HIST;
+    }
     return AQ_OK;
 }
 
@@ -1114,18 +401,16 @@ void fill_result(const HostOut& h, aq_result* out) {
 }
 
 int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
-    const size_t nbytes = offsetof(SlotOut, wg) + sizeof(WgPart) * (size_t)ctx->persist_grid;
-    AQ_HIP(hipMemcpyAsync(ctx->h_slot, ctx->d_out + slot, nbytes, hipMemcpyDeviceToHost, ctx->stream));
+    AQ_HIP(hipMemcpyAsync(ctx->h_parts, ctx->d_parts + (size_t)slot * ctx->grid, sizeof(WgPart) * (size_t)ctx->grid,
+                          hipMemcpyDeviceToHost, ctx->stream));
     if (ctx->slot_hist[slot])
         AQ_HIP(hipMemcpyAsync(ctx->h_hist, ctx->d_ctl[slot].hist, sizeof(unsigned long long) * 2 * AQ_MAX_LEVELS,
                               hipMemcpyDeviceToHost, ctx->stream));
     AQ_HIP(hipStreamSynchronize(ctx->stream));
-    const SlotOut& s = *ctx->h_slot;
     HostOut& h = ctx->last;
     h = HostOut();
-    const unsigned nwg = std::min<unsigned>(s.nwg, MAXG);
-    for (unsigned i = 0; i < nwg; ++i) {
-        const WgPart& w = s.wg[i];
+    for (int i = 0; i < ctx->grid; ++i) {
+        const WgPart& w = ctx->h_parts[i];
         h.area += w.area;
         h.tasks += w.tasks;
         h.leaves += w.leaves;
@@ -1138,6 +423,16 @@ int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
     ctx->last_valid = true;
     fill_result(h, out);
     return err_from_bits(h.error);
+}
+
+int launch_any(aq_ctx* ctx, int integrand, int k, const double* a, const double* b, double eps, int max_depth,
+               int shard, int nshards, int first_slot) {
+    const bool h = ctx->histograms;
+    if (integrand == AQ_F_COSH4)
+        return h ? launch_stream<F_COSH4, true>(ctx, k, a, b, eps, max_depth, shard, nshards, first_slot)
+                 : launch_stream<F_COSH4, false>(ctx, k, a, b, eps, max_depth, shard, nshards, first_slot);
+    return h ? launch_stream<F_SIN_RECIP, true>(ctx, k, a, b, eps, max_depth, shard, nshards, first_slot)
+             : launch_stream<F_SIN_RECIP, false>(ctx, k, a, b, eps, max_depth, shard, nshards, first_slot);
 }
 
 }  // namespace
@@ -1179,25 +474,27 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipGetDeviceProperties(&prop, device));
     c->num_cus = prop.multiProcessorCount;
     int occ = 0;
-    AQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_persist<F_COSH4, true, false>, PT, 0));
+    AQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_stream<F_COSH4, true, false>, PT, 0));
     if (occ < 1) {
         delete c;
         return AQ_ENODEV;
     }
-    // One workgroup per CU: the LDS stack takes most of the CU's LDS; residency of the whole grid
-    // is required by the token protocol (idle workgroups wait for busy ones).
-    c->persist_grid = std::min(c->num_cus, MAXG);
+    // One workgroup per CU (the LDS rings take most of a CU's LDS); the whole grid must be
+    // resident, because idle workgroups wait on the queue for busy ones.
+    c->grid = std::min(c->num_cus, MAXG);
     AQ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     AQ_HIP(hipMalloc(&c->d_tab, sizeof(ExpEntry) * 128));
     AQ_HIP(hipMemcpy(c->d_tab, aq_exp_tab_host, sizeof(ExpEntry) * 128, hipMemcpyHostToDevice));
     AQ_HIP(hipMalloc(&c->d_ctl, sizeof(Ctl) * NSLOTS));
     AQ_HIP(hipMemset(c->d_ctl, 0, sizeof(Ctl) * NSLOTS));
-    AQ_HIP(hipMalloc(&c->d_out, sizeof(SlotOut) * NSLOTS));
-    AQ_HIP(hipMemset(c->d_out, 0, sizeof(SlotOut) * NSLOTS));
+    AQ_HIP(hipMalloc(&c->d_parts, sizeof(WgPart) * (size_t)NSLOTS * c->grid));
+    AQ_HIP(hipMemset(c->d_parts, 0, sizeof(WgPart) * (size_t)NSLOTS * c->grid));
+    AQ_HIP(hipMalloc(&c->d_bounds, sizeof(double2) * NSLOTS));
+    AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS, hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_chunks, sizeof(Chunk) * (size_t)QCAP));
-    AQ_HIP(hipMalloc(&c->d_ready, sizeof(unsigned) * (size_t)QCAP));
-    AQ_HIP(hipMemset(c->d_ready, 0, sizeof(unsigned) * (size_t)QCAP));
-    AQ_HIP(hipHostMalloc(&c->h_slot, sizeof(SlotOut), hipHostMallocDefault));
+    AQ_HIP(hipMalloc(&c->d_ready, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
+    AQ_HIP(hipMemset(c->d_ready, 0, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
+    AQ_HIP(hipHostMalloc(&c->h_parts, sizeof(WgPart) * (size_t)c->grid, hipHostMallocDefault));
     AQ_HIP(hipHostMalloc(&c->h_hist, sizeof(unsigned long long) * 2 * AQ_MAX_LEVELS, hipHostMallocDefault));
     AQ_HIP(hipHostMalloc(&c->h_lres, sizeof(DevResults), hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_lres, sizeof(DevResults)));
@@ -1215,7 +512,8 @@ void aq_ctx_destroy(aq_ctx* c) {
     for (auto& e : c->ev_free) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     (void)hipFree(c->d_tab);
     (void)hipFree(c->d_ctl);
-    (void)hipFree(c->d_out);
+    (void)hipFree(c->d_parts);
+    (void)hipFree(c->d_bounds);
     (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_ready);
     (void)hipFree(c->d_lres);
@@ -1225,7 +523,8 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_count);
     (void)hipFree(c->d_x);
     (void)hipFree(c->d_y);
-    if (c->h_slot) (void)hipHostFree(c->h_slot);
+    if (c->h_bounds) (void)hipHostFree(c->h_bounds);
+    if (c->h_parts) (void)hipHostFree(c->h_parts);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->h_lres) (void)hipHostFree(c->h_lres);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1257,7 +556,7 @@ int aq_set_diagnostics(aq_ctx* c, int enable) {
 int aq_diagnostics(aq_ctx* c, uint64_t* out, int cap_words) {
     if (!c || !out || !c->d_diag) return AQ_EINVAL;
     AQ_HIP(hipSetDevice(c->device));
-    const size_t words = std::min<size_t>((size_t)cap_words, (size_t)DIAG_WORDS * c->persist_grid);
+    const size_t words = std::min<size_t>((size_t)cap_words, (size_t)DIAG_WORDS * c->grid);
     AQ_HIP(hipStreamSynchronize(c->stream));
     AQ_HIP(hipMemcpy(out, c->d_diag, words * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return (int)(words / DIAG_WORDS);
@@ -1265,25 +564,33 @@ int aq_diagnostics(aq_ctx* c, uint64_t* out, int cap_words) {
 
 int aq_async_slots(void) { return NSLOTS; }
 
+int aq_max_integrals_per_launch(void) { return MAXK; }
+
+int aq_integrate_many_async(aq_ctx* ctx, int integrand, int k, const double* a, const double* b, double eps,
+                            int max_depth, int shard, int nshards, int first_slot) {
+    if (!ctx || k < 1 || k > MAXK || !a || !b) return AQ_EINVAL;
+    if (integrand != AQ_F_COSH4 && integrand != AQ_F_SIN_RECIP) return AQ_EINVAL;
+    if (!(eps >= 0.0) || max_depth < 0 || max_depth > AQ_MAX_LEVELS - 1) return AQ_EINVAL;
+    if (nshards < 1 || shard < 0 || shard >= nshards || nshards > 64) return AQ_EINVAL;
+    if (first_slot < 0 || first_slot + k > NSLOTS) return AQ_EINVAL;
+    for (int i = 0; i < k; ++i)
+        if (!bounds_ok(a[i], b[i])) return AQ_EINVAL;
+    AQ_HIP(hipSetDevice(ctx->device));
+    return launch_any(ctx, integrand, k, a, b, eps, max_depth, shard, nshards, first_slot);
+}
+
 int aq_integrate_async(aq_ctx* ctx, const aq_problem* p, int shard, int nshards, int slot) {
     if (!ctx) return AQ_EINVAL;
     int rc = validate(p);
     if (rc) return rc;
-    if (nshards < 1 || shard < 0 || shard >= nshards || nshards > 64) return AQ_EINVAL;
-    if (slot < 0 || slot >= NSLOTS) return AQ_EINVAL;
-    AQ_HIP(hipSetDevice(ctx->device));
-    if (p->integrand == AQ_F_COSH4)
-        return ctx->histograms ? launch_persist<F_COSH4, true>(ctx, p, shard, nshards, slot)
-                               : launch_persist<F_COSH4, false>(ctx, p, shard, nshards, slot);
-    return ctx->histograms ? launch_persist<F_SIN_RECIP, true>(ctx, p, shard, nshards, slot)
-                           : launch_persist<F_SIN_RECIP, false>(ctx, p, shard, nshards, slot);
+    return aq_integrate_many_async(ctx, p->integrand, 1, &p->a, &p->b, p->eps, p->max_depth, shard, nshards, slot);
 }
 
 int aq_gather_results(aq_ctx* ctx, int first_slot, int n, void* d_out) {
     if (!ctx || !d_out || n < 0 || n > NSLOTS || first_slot < 0 || first_slot >= NSLOTS) return AQ_EINVAL;
     if (n == 0) return AQ_OK;
     AQ_HIP(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_out, first_slot, n, NSLOTS,
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_parts, ctx->grid, first_slot, n, NSLOTS,
                        (double*)d_out);
     AQ_HIP(hipGetLastError());
     return AQ_OK;
@@ -1437,28 +744,27 @@ int aq_eval_cosh(aq_ctx* ctx, size_t n, const double* x, double* out) {
 
 int aq_integrate_batch(aq_ctx* ctx, int integrand, size_t n, const double* a, const double* b, double eps,
                        double* area, uint64_t* tasks, uint64_t* accepted) {
-    // Round-1 batch front end: the integrals are pipelined through the persistent path, up to
-    // NSLOTS launches in flight, no host synchronisation between them.
+    // Batch front end (SURVEY config 3): MAXK integrals per persistent launch, every integral with
+    // its own slot and per-workgroup partials; launches are pipelined on the context's stream.
     if (!ctx || (n && (!a || !b))) return AQ_EINVAL;
+    for (size_t i = 0; i < n; ++i)
+        if (!bounds_ok(a[i], b[i])) return AQ_EINVAL;
     const bool hist = ctx->histograms;
     ctx->histograms = false;
     int rc = AQ_OK;
     size_t done = 0;
     while (done < n && rc == AQ_OK) {
-        const size_t m = std::min<size_t>(n - done, NSLOTS);
-        for (size_t i = 0; i < m && rc == AQ_OK; ++i) {
-            aq_problem p{integrand, 0, a[done + i], b[done + i], eps};
-            rc = aq_integrate_async(ctx, &p, 0, 1, (int)i);
-        }
-        for (size_t i = 0; i < m && rc == AQ_OK; ++i) {
+        const int m = (int)std::min<size_t>(n - done, (size_t)MAXK);
+        rc = aq_integrate_many_async(ctx, integrand, m, a + done, b + done, eps, 0, 0, 1, 0);
+        for (int i = 0; i < m && rc == AQ_OK; ++i) {
             aq_result r{};
-            rc = aq_fetch(ctx, (int)i, &r);
+            rc = aq_fetch(ctx, i, &r);
             if (rc) break;
             if (area) area[done + i] = r.area;
             if (tasks) tasks[done + i] = r.tasks;
             if (accepted) accepted[done + i] = r.accepted;
         }
-        done += m;
+        done += (size_t)m;
     }
     ctx->histograms = hist;
     return rc;

@@ -119,7 +119,8 @@ def test_shards_match_oracle_partition(ctx, trees, oracle, name, nshards):
     area = 0.0
     for s in range(nshards):
         r = ctx.integrate_shard(p, s, nshards)
-        o = oracle.integrate_shard(s, nshards, G=ctx.num_cus, integrand=p.integrand, a=p.a, b=p.b, eps=p.eps)
+        o = oracle.integrate_shard(s, nshards, G=ctx.num_cus * 8, S=2, integrand=p.integrand, a=p.a, b=p.b,
+                                   eps=p.eps)
         assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
         assert r.tasks_per_level == o.tasks_per_level
         tot_t += r.tasks
@@ -181,3 +182,44 @@ def test_cli_reference_output(trees):
     assert lines[3] == "0\t1\t2\t3\t4\t"
     counts = [int(v) for v in lines[4].split()]
     assert counts[0] == 0 and sum(counts) == 6567
+
+
+def test_many_integrals_one_launch(ctx, oracle, trees):
+    """K integrals with different bounds share one persistent launch; each slot is its own tree."""
+    a, b = oracle.batch_bounds(7)
+    a = np.concatenate([[0.0], a, [0.0]])
+    b = np.concatenate([[5.0], b, [5.0]])
+    ctx.integrate_many_async(a, b, 1e-8, first_slot=3)
+    for i in range(a.size):
+        r = ctx.fetch(3 + i, detail=True)
+        o = oracle.integrate(a=a[i], b=b[i], eps=1e-8)
+        assert (r.tasks, r.accepted, r.levels) == (o.tasks, o.leaves, o.levels)
+        assert r.tasks_per_level == o.tasks_per_level and r.leaves_per_level == o.leaves_per_level
+        assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
+
+
+def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
+    k = ctx.max_integrals_per_launch
+    a, b = oracle.batch_bounds(k)
+    ctx.set_level_histograms(False)
+    try:
+        ctx.integrate_many_async(a, b, 1e-3, first_slot=0)
+        got = [ctx.fetch(i) for i in range(k)]
+    finally:
+        ctx.set_level_histograms(True)
+    assert [g.accepted for g in got] == batch_golden["leaves_eps1e-3_first256"][:k]
+    want = [float.fromhex(h) for h in batch_golden["area_eps1e-3_first256_hex"][:k]]
+    assert all(abs(g.area - w) <= AREA_RTOL * abs(w) for g, w in zip(got, want))
+
+
+def test_many_sharded(ctx, oracle, trees):
+    """Sharded multi-integral launches: per-shard counts match the oracle partition (G*8 wave workers)."""
+    g = trees["cosh4_eps1e-10"]
+    tot_t = tot_l = 0
+    for s in range(2):
+        ctx.integrate_many_async(np.zeros(3), np.full(3, 5.0), 1e-10, first_slot=10, shard=s, nshards=2)
+        rs = [ctx.fetch(10 + i) for i in range(3)]
+        assert len({(r.tasks, r.accepted) for r in rs}) == 1
+        tot_t += rs[0].tasks
+        tot_l += rs[0].accepted
+    assert (tot_t, tot_l) == (g["tasks"], g["leaves"])

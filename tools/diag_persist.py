@@ -29,9 +29,14 @@ def summarize(d, f):
     s["cyc_per_round"] = float(np.median(col["c_round"] / r))
     s["cyc_eval_per_round"] = float(np.median(col["c_eval"] / r))
     s["cyc_seed_p50"] = float(np.median(col["c_seed"]))
+    for k in ("c_seed1", "c_seed2", "c_seed3"):
+        s["cyc_" + k[2:] + "_p50"] = float(np.median(col[k]))
+    s["cyc_idle_per_wg_p50"] = float(np.median(col["c_idle"]))
+    s["cyc_share_per_wg_p50"] = float(np.median(col["c_share"]))
+    s["give_records"] = col["give"].sum()
     s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
                   "sum": col["tasks"].sum()}
-    for k in ("leads", "pool_push", "pool_take", "lock_spins", "spill_records", "chunks_out", "chunks_in",
+    for k in ("leads", "pool_push", "pool_take", "give", "lock_spins", "spill_records", "chunks_out", "chunks_in",
               "records_out", "records_in"):
         s[k] = {"sum": col[k].sum(), "max": col[k].max()}
     s["t_wait_us_p50"] = float(np.median(col["t_wait"])) / 100.0
