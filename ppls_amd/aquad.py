@@ -188,7 +188,7 @@ class Context:
     DIAG_FIELDS = ("t_start", "t_seeded", "t_first_lead", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
                    "records_out", "t_wait", "leads", "seeds", "pool_push", "cu", "records_in", "active_lanes",
                    "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed",
-                   "c_seed1", "c_seed2", "c_seed3", "c_idle", "c_lock", "c_share", "give", "pad")
+                   "seed_calls", "c_seed_resolve", "mixed_rounds", "c_idle", "c_seed_pass1", "c_seed_pass2", "give", "pad")
     DIAG_WORDS = 32
 
     def set_diagnostics(self, enable: bool):

@@ -195,6 +195,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     __shared__ ExpEntry tab[128];
     __shared__ WgState S;
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
+    __shared__ double2 s_bounds[MAXK];   // {a, b} of every integral of the launch
 
     const unsigned tid = threadIdx.x;
     const unsigned lane = lane_id();
@@ -209,8 +210,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
-    if (tid < (unsigned)P.nprob && tid < (unsigned)MAXK)
+    if (tid < (unsigned)P.nprob && tid < (unsigned)MAXK) {
         P.parts[(size_t)(P.first_slot + tid) * gridDim.x + blockIdx.x].cu = cu_slot();
+        s_bounds[tid] = P.bounds[tid];
+    }
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
@@ -222,6 +225,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per wave (<= 8)
     const unsigned npairs = (unsigned)D * nb;
     const unsigned base = wid * WCAP;                            // this wave's ring
+    // seeding fast path (npairs <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
+    unsigned long long colmask = 0;
+    if (npairs <= 64) {
+        const unsigned kk = lane % nb;
+        for (int d = 0; d < D; ++d)
+            if ((unsigned)d * nb + kk < 64u) colmask |= 1ull << ((unsigned)d * nb + kk);
+    }
 
     Acc acc{0.0, 0u, 0u, 0u};
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
@@ -308,7 +318,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     flush_acc(P, acc, tag, lane);
                     tag = p;
                 }
-                const double2 ab = P.bounds[p];
+                const double2 ab = s_bounds[p];
                 const double A = ab.x, B = ab.y;
                 double* fm = s_l + base;          // [npairs + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
                 double* leafa = s_r + base;       // [npairs]: larea + rarea of node (d,k)
@@ -319,84 +329,142 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     valid = j < npos_total;
                     return j;
                 };
-                for (unsigned q0 = 0; q0 < npairs + 2; q0 += 64) {
-                    const unsigned q = q0 + lane;
-                    if (q < npairs + 2) {
-                        double x;
+                unsigned long long cp1 = 0, cp2 = 0;
+                bool alive = false;
+                double l = A, r = B, fl = 0.0, fr = 0.0;
+                if (npairs <= 64) {
+                    // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
+                    // decision; the first leaf depth of every position comes from ONE ballot
+                    const unsigned q = lane;
+                    const bool isnode = q < npairs;
+                    const unsigned d = isnode ? q / nb : 0u, kk = isnode ? q - d * nb : 0u;
+                    bool valid = false;
+                    const unsigned long long pp = isnode ? position(kk, valid) : 0ull;
+                    const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
+                    unsigned li = npairs, ri = npairs + 1;
+                    for (unsigned i = 0; i < d; ++i) {
+                        const double m = (l + r) / 2;
+                        if ((anc >> (d - 1 - i)) & 1ull) { l = m; li = i * nb + kk; } else { r = m; ri = i * nb + kk; }
+                    }
+                    const double mid = (l + r) / 2;                           // :187
+                    const unsigned fq = npairs + 2 <= 64 ? q : (q < npairs ? q : 64u);
+                    double fmid = 0.0;
+                    if (fq < npairs + 2)
+                        fmid = integrand<FID>(isnode ? mid : (q == npairs ? A : B), tab);   // :188
+                    if (fq < npairs + 2) fm[q] = fmid;
+                    if (npairs + 2 > 64 && lane < 2) fm[npairs + lane] = integrand<FID>(lane == 0 ? A : B, tab);
+                    if constexpr (DIAG) cp1 = clk();
+                    bool refine = false;
+                    double leafarea = 0.0;
+                    if (isnode) {
+                        fl = fm[li];
+                        fr = fm[ri];
+                        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
+                        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
+                        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
+                        refine = fabs((larea + rarea) - lrarea) > eps;       // :191
+                        leafarea = larea + rarea;                             // :199
+                    }
+                    const unsigned long long leafm = __ballot(isnode && valid && !refine) & colmask;
+                    const unsigned dstar = leafm ? (unsigned)__builtin_ctzll(leafm) / nb : (unsigned)D;
+                    if (isnode && valid && d <= dstar && (pp & ((1ull << (D - (int)d)) - 1ull)) == 0ull) {
+                        ++acc.tasks;                                          // owner of node (d, kk)
+                        acc.maxd = max(acc.maxd, d + 1u);
+                        if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
+                        if (d == dstar) {
+                            acc.area += leafarea;                             // :199 -> :149
+                            ++acc.leaves;
+                            if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
+                        } else if ((int)d + 1 >= max_depth) {
+                            err |= ERRB_DEPTH;
+                        }
+                    }
+                    // the depth-(D-1) node of a surviving path emits the position's depth-D record
+                    alive = isnode && valid && (int)d == D - 1 && dstar >= (unsigned)D && D < max_depth;
+                    if (alive) {
+                        if (pp & 1ull) { l = mid; fl = fmid; } else { r = mid; fr = fmid; }
+                    }
+                    if constexpr (DIAG) cp2 = clk();
+                } else {
+                    for (unsigned q0 = 0; q0 < npairs + 2; q0 += 64) {
+                        const unsigned q = q0 + lane;
+                        if (q < npairs + 2) {
+                            double x;
+                            if (q < npairs) {
+                                const unsigned d = q / nb, kk = q % nb;
+                                bool valid;
+                                const unsigned long long pp = position(kk, valid);
+                                const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
+                                double ll = A, rr = B;
+                                for (unsigned i = 0; i < d; ++i) {
+                                    const double m = (ll + rr) / 2;
+                                    if ((anc >> (d - 1 - i)) & 1ull) ll = m; else rr = m;
+                                }
+                                x = (ll + rr) / 2;
+                            } else {
+                                x = (q == npairs) ? A : B;
+                            }
+                            fm[q] = integrand<FID>(x, tab);
+                        }
+                    }
+                    if constexpr (DIAG) cp1 = clk();
+                    for (unsigned q0 = 0; q0 < npairs; q0 += 64) {
+                        const unsigned q = q0 + lane;
                         if (q < npairs) {
                             const unsigned d = q / nb, kk = q % nb;
                             bool valid;
                             const unsigned long long pp = position(kk, valid);
                             const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
-                            double l = A, r = B;
+                            double ll = A, rr = B;
+                            unsigned li = npairs, ri = npairs + 1;
                             for (unsigned i = 0; i < d; ++i) {
+                                const double m = (ll + rr) / 2;
+                                if ((anc >> (d - 1 - i)) & 1ull) { ll = m; li = i * nb + kk; } else { rr = m; ri = i * nb + kk; }
+                            }
+                            const double fll = fm[li], frr = fm[ri], fmid = fm[q];
+                            const double mid = (ll + rr) / 2;
+                            const double lrarea = (fll + frr) * (rr - ll) / 2;    // :185
+                            const double larea = (fll + fmid) * (mid - ll) / 2;   // :189
+                            const double rarea = (fmid + frr) * (rr - mid) / 2;   // :190
+                            flag[q] = fabs((larea + rarea) - lrarea) > eps ? 1u : 0u;   // :191
+                            leafa[q] = larea + rarea;                             // :199
+                        }
+                    }
+                    if constexpr (DIAG) cp2 = clk();
+                    // resolve: lane kk < nb follows position kk down its path
+                    const unsigned kk = lane;
+                    bool valid = false;
+                    const unsigned long long pp = (kk < nb) ? position(kk, valid) : 0ull;
+                    unsigned long long fmask = 0;
+                    for (int d = 0; d < D; ++d)
+                        fmask |= (unsigned long long)(flag[(unsigned)d * nb + (kk < nb ? kk : 0u)] & 1u) << d;
+                    const int dstar = (int)__builtin_ctzll(~fmask);   // first depth that does not refine (D if none)
+                    if (valid) {
+                        const int dlast = min(dstar, D - 1);
+                        for (int d = 0; d <= dlast; ++d) {
+                            if ((pp & ((1ull << (D - d)) - 1ull)) == 0ull) {   // owner of node (d, kk)
+                                ++acc.tasks;
+                                acc.maxd = max(acc.maxd, (unsigned)d + 1u);
+                                if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
+                                if (d == dstar) {
+                                    acc.area += leafa[(unsigned)d * nb + kk];          // :199 -> :149
+                                    ++acc.leaves;
+                                    if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
+                                } else if (d + 1 >= max_depth) {
+                                    err |= ERRB_DEPTH;
+                                }
+                            }
+                        }
+                        alive = dstar >= D && D < max_depth;
+                        if (alive) {
+                            unsigned li = npairs, ri = npairs + 1;
+                            for (int i = 0; i < D; ++i) {
                                 const double m = (l + r) / 2;
-                                if ((anc >> (d - 1 - i)) & 1ull) l = m; else r = m;
+                                if ((pp >> (D - 1 - i)) & 1ull) { l = m; li = (unsigned)i * nb + kk; } else { r = m; ri = (unsigned)i * nb + kk; }
                             }
-                            x = (l + r) / 2;
-                        } else {
-                            x = (q == npairs) ? A : B;
+                            fl = fm[li];
+                            fr = fm[ri];
                         }
-                        fm[q] = integrand<FID>(x, tab);
-                    }
-                }
-                for (unsigned q0 = 0; q0 < npairs; q0 += 64) {
-                    const unsigned q = q0 + lane;
-                    if (q < npairs) {
-                        const unsigned d = q / nb, kk = q % nb;
-                        bool valid;
-                        const unsigned long long pp = position(kk, valid);
-                        const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
-                        double l = A, r = B;
-                        unsigned li = npairs, ri = npairs + 1;
-                        for (unsigned i = 0; i < d; ++i) {
-                            const double m = (l + r) / 2;
-                            if ((anc >> (d - 1 - i)) & 1ull) { l = m; li = i * nb + kk; } else { r = m; ri = i * nb + kk; }
-                        }
-                        const double fl = fm[li], fr = fm[ri], fmid = fm[q];
-                        const double mid = (l + r) / 2;
-                        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
-                        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
-                        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
-                        flag[q] = fabs((larea + rarea) - lrarea) > eps ? 1u : 0u;   // :191
-                        leafa[q] = larea + rarea;                             // :199
-                    }
-                }
-                // resolve: lane kk < nb follows position kk down its path
-                const unsigned kk = lane;
-                bool valid = false;
-                const unsigned long long pp = (kk < nb) ? position(kk, valid) : 0ull;
-                unsigned long long fmask = 0;
-                for (int d = 0; d < D; ++d)
-                    fmask |= (unsigned long long)(flag[(unsigned)d * nb + (kk < nb ? kk : 0u)] & 1u) << d;
-                const int dstar = (int)__builtin_ctzll(~fmask);   // first depth that does not refine (D if none)
-                bool alive = false;
-                double l = A, r = B, fl = 0.0, fr = 0.0;
-                if (valid) {
-                    const int dlast = min(dstar, D - 1);
-                    for (int d = 0; d <= dlast; ++d) {
-                        if ((pp & ((1ull << (D - d)) - 1ull)) == 0ull) {   // owner of node (d, kk)
-                            ++acc.tasks;
-                            acc.maxd = max(acc.maxd, (unsigned)d + 1u);
-                            if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
-                            if (d == dstar) {
-                                acc.area += leafa[(unsigned)d * nb + kk];          // :199 -> :149
-                                ++acc.leaves;
-                                if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
-                            } else if (d + 1 >= max_depth) {
-                                err |= ERRB_DEPTH;
-                            }
-                        }
-                    }
-                    alive = dstar >= D && D < max_depth;
-                    if (alive) {
-                        unsigned li = npairs, ri = npairs + 1;
-                        for (int i = 0; i < D; ++i) {
-                            const double m = (l + r) / 2;
-                            if ((pp >> (D - 1 - i)) & 1ull) { l = m; li = (unsigned)i * nb + kk; } else { r = m; ri = (unsigned)i * nb + kk; }
-                        }
-                        fl = fm[li];
-                        fr = fm[ri];
                     }
                 }
                 __builtin_amdgcn_wave_barrier();   // every read of the scratch precedes the seed writes
@@ -410,6 +478,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if constexpr (DIAG) {
                     if (lane == 0) {
                         atomicAdd(&s_dg[DG_SEED_CALLS], 1ull);
+                        atomicAdd(&s_dg[DG_C_LOCK], cp1 - cs);
+                        atomicAdd(&s_dg[DG_C_SHARE], cp2 - cp1);
+                        atomicAdd(&s_dg[DG_FLUSHES], clk() - cp2);
                         atomicAdd(&s_dg[DG_SEEDS], (unsigned long long)top);
                         atomicAdd(&s_dg[DG_C_SEED], clk() - cs);
                         atomicMax(&s_dg[DG_T_SEEDED], rtc());

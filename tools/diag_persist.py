@@ -28,16 +28,16 @@ def summarize(d, f):
     s["lanes_per_round"] = float(col["active_lanes"].sum() / max(col["rounds"].sum(), 1))
     s["cyc_per_round"] = float(np.median(col["c_round"] / r))
     s["cyc_eval_per_round"] = float(np.median(col["c_eval"] / r))
-    s["cyc_seed_p50"] = float(np.median(col["c_seed"]))
-    for k in ("c_seed1", "c_seed2", "c_seed3"):
-        s["cyc_" + k[2:] + "_p50"] = float(np.median(col[k]))
+    s["cyc_seed_per_call"] = float(col["c_seed"].sum() / max(col["seed_calls"].sum(), 1))
+    for k in ("c_seed_pass1", "c_seed_pass2", "c_seed_resolve"):
+        s["cyc_" + k[2:] + "_per_call"] = float(col[k].sum() / max(col["seed_calls"].sum(), 1))
     s["cyc_idle_per_wg_p50"] = float(np.median(col["c_idle"]))
-    s["cyc_share_per_wg_p50"] = float(np.median(col["c_share"]))
-    s["give_records"] = col["give"].sum()
+    s["cyc_round_per_wg_p50"] = float(np.median(col["c_round"]))
+    s["cyc_seed_per_wg_p50"] = float(np.median(col["c_seed"]))
     s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
                   "sum": col["tasks"].sum()}
     for k in ("leads", "pool_push", "pool_take", "give", "lock_spins", "spill_records", "chunks_out", "chunks_in",
-              "records_out", "records_in"):
+              "records_out", "records_in", "seed_calls", "mixed_rounds"):
         s[k] = {"sum": col[k].sum(), "max": col[k].max()}
     s["t_wait_us_p50"] = float(np.median(col["t_wait"])) / 100.0
     s["max_ring"] = col["max_ring"].max()
@@ -50,16 +50,21 @@ def main():
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--k", type=int, default=1, help="integrals per launch")
     args = ap.parse_args()
     ctx = Context(0)
     ctx.set_level_histograms(False)
     ctx.set_diagnostics(True)
     res = []
     for _ in range(args.reps):
-        r = ctx.integrate(Problem(eps=args.eps))
+        if args.k == 1:
+            r = ctx.integrate(Problem(eps=args.eps))
+        else:
+            ctx.integrate_many_async(np.zeros(args.k), np.full(args.k, 5.0), args.eps)
+            r = ctx.fetch(args.k - 1)
         d, f = ctx.diagnostics()
         res.append(summarize(d, f))
-    print(json.dumps({"eps": args.eps, "tasks": r.tasks, "accepted": r.accepted, "summary": res[-1]}, indent=1,
+    print(json.dumps({"eps": args.eps, "k": args.k, "tasks": r.tasks, "accepted": r.accepted, "summary": res[-1]}, indent=1,
                      default=float))
     if args.out:
         np.save(args.out.replace(".json", ".npy"), d)
