@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip the one-integral-per-launch latency probe (profiling runs: every dispatch is K-wide)")
     ap.add_argument("--per-launch", type=int, default=256,
                     help="integrals per persistent launch (1 = one launch per integral)")
     args = ap.parse_args()
@@ -128,12 +130,14 @@ def main():
         ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank, nshards=world)
 
     # single-integral latency (one integral per launch), reported beside the throughput
-    ctx.kernel_timing(True)
-    for _ in range(max(args.warmup, 5)):
-        launch(1)
-    ctx.synchronize()
-    single_ms, single_n = ctx.kernel_time()
-    ctx.kernel_timing(False)
+    single_ms, single_n = 0.0, 0
+    if not args.no_single:
+        ctx.kernel_timing(True)
+        for _ in range(max(args.warmup, 5)):
+            launch(1)
+        ctx.synchronize()
+        single_ms, single_n = ctx.kernel_time()
+        ctx.kernel_timing(False)
 
     # warmup (also validates)
     for _ in range(max(1, args.warmup // kmax)):
@@ -209,7 +213,7 @@ def main():
                        "parallelism": f"shard{world}" if world > 1 else "single-gpu",
                        "integrals_per_launch": per_launch,
                        "workgroups_per_gpu": ctx.num_cus},
-            "single_integral_kernel_us": single_ms * 1e3 / max(single_n, 1),
+            "single_integral_kernel_us": single_ms * 1e3 / single_n if single_n else None,
             "verified": ok,
             "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(),

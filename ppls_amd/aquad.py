@@ -188,14 +188,15 @@ class Context:
     DIAG_FIELDS = ("t_start", "t_seeded", "t_first_lead", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
                    "records_out", "t_wait", "leads", "seeds", "pool_push", "cu", "records_in", "active_lanes",
                    "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed",
-                   "seed_calls", "c_seed_resolve", "mixed_rounds", "c_idle", "c_seed_pass1", "c_seed_pass2", "give", "pad")
-    DIAG_WORDS = 32
+                   "seed_calls", "c_seed_resolve", "mixed_rounds", "c_idle", "c_seed_pass1", "c_seed_pass2", "give", "cellar_in",
+                   "cellar_out", "pad33", "pad34", "pad35", "pad36", "pad37", "pad38", "pad39")
+    DIAG_WORDS = 40
 
     def set_diagnostics(self, enable: bool):
         _check(self.L.aq_set_diagnostics(self._h, 1 if enable else 0), "aq_set_diagnostics")
 
     def diagnostics(self):
-        """Per-workgroup timeline of the last persistent launch: numpy (n_wg, 16) uint64 + field names."""
+        """Per-workgroup timeline of the last persistent launch: numpy (n_wg, DIAG_WORDS) uint64 + field names."""
         w = self.DIAG_WORDS
         out = np.zeros(w * 2048, np.uint64)
         n = self.L.aq_diagnostics(self._h, _up(out), out.size)

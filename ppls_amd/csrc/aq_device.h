@@ -64,6 +64,27 @@ __device__ __forceinline__ Step task_step(double l, double r, double fl, double 
     return s;
 }
 
+// K trapezoid steps at once (K records per lane); every lane of the wave calls it (inactive lanes
+// pass a harmless record, e.g. l = r = 1, F = 0).
+template <int FID, int K>
+__device__ __forceinline__ void task_step_k(const double (&l)[K], const double (&r)[K], const double (&fl)[K],
+                                            const double (&fr)[K], double eps, const ExpEntry* __restrict__ tab,
+                                            Step (&s)[K]) {
+    double mid[K], fmid[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) mid[k] = (l[k] + r[k]) / 2;   // :187
+    integrand_k<FID, K>(mid, fmid, tab);                       // :188
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double lrarea = (fl[k] + fr[k]) * (r[k] - l[k]) / 2;   // :185
+        s[k].mid = mid[k];
+        s[k].fmid = fmid[k];
+        s[k].larea = (fl[k] + fmid[k]) * (mid[k] - l[k]) / 2;         // :189
+        s[k].rarea = (fmid[k] + fr[k]) * (r[k] - mid[k]) / 2;         // :190
+        s[k].refine = fabs((s[k].larea + s[k].rarea) - lrarea) > eps;  // :191
+    }
+}
+
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
 
 __device__ __forceinline__ unsigned long long clk() {

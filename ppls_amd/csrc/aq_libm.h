@@ -81,6 +81,22 @@ __device__ __forceinline__ double expm1_glibc_small(double x) {
     return x - (x * e - hxs);
 }
 
+// RN(0.5 / t) for 1 <= t < 2^64 -- the instruction sequence the compiler emits for the IEEE division
+// (v_rcp_f64, two Newton steps, quotient, residual, fused correction) without v_div_scale /
+// v_div_fmas / v_div_fixup, which are identities in this range (no operand needs rescaling, no
+// special value). They are dropped because v_div_scale / v_div_fmas pass a flag through VCC, and
+// that single register serialises any two divisions a wave would otherwise overlap.
+__device__ __forceinline__ double half_recip(double t) {
+    double y = __builtin_amdgcn_rcp(t);
+    double e = __fma_rn(-t, y, 1.0);
+    y = __fma_rn(y, e, y);
+    e = __fma_rn(-t, y, 1.0);
+    y = __fma_rn(y, e, y);
+    const double q = 0.5 * y;
+    const double r = __fma_rn(-t, q, 0.5);
+    return __fma_rn(r, y, q);
+}
+
 // glibc __ieee754_cosh.
 __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restrict__ tab) {
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
@@ -93,7 +109,7 @@ __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restric
             return 1.0 + (t * t) / (w + w);
         }
         const double t = exp_glibc(ax, tab);
-        return 0.5 * t + 0.5 / t;
+        return 0.5 * t + half_recip(t);     // 0.5 / t, t in [1.41, 3.6e9]
     }
     if (ix >= 0x7ff00000u) return x * x;
     if (ix < 0x40862e42u) return 0.5 * exp_glibc(ax, tab);
@@ -118,6 +134,78 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
         // SURVEY config 4: sin(1/x). Leaf counts are insensitive to +-1 ulp in sin,
         // so the device libm's faithful sin is used.
         return sin(1.0 / x);
+    }
+}
+
+// cosh for K independent arguments, written stage by stage so the K dependency chains interleave
+// (the main path has no branch). c[k] is exact for 0.5*ln2 <= |x[k]| < 22; the return value is a
+// lane flag set when some x[k] is outside that range, for the caller to redo with cosh_glibc.
+__device__ __forceinline__ bool cosh_main_range(double x) {
+    const uint32_t ix = hi_word(x) & 0x7fffffffu;
+    return ix >= 0x3fd62e43u && ix < 0x40360000u;
+}
+template <int K>
+__device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab) {
+    double ax[K], kd[K], r[K], r2[K], tmp[K], t[K];
+    uint64_t ki[K];
+    ExpEntry e[K];
+    bool out = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        ax[k] = fabs(x[k]);
+        kd[k] = __fma_rn(kInvLn2N, ax[k], kShift);
+        ki[k] = (uint64_t)__double_as_longlong(kd[k]);
+        e[k] = tab[ki[k] & 127];
+        out |= !cosh_main_range(x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        kd[k] = kd[k] - kShift;
+        r[k] = __fma_rn(kd[k], kNegLn2loN, __fma_rn(kd[k], kNegLn2hiN, ax[k]));
+        r2[k] = r[k] * r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double tail = __longlong_as_double((long long)e[k].tail_bits);
+        tmp[k] = __fma_rn(r2[k] * r2[k], __fma_rn(r[k], kC5, kC4), __fma_rn(r2[k], __fma_rn(r[k], kC3, kC2), tail + r[k]));
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double scale = __longlong_as_double((long long)(e[k].sbits + (ki[k] << 45)));
+        t[k] = __fma_rn(scale, tmp[k], scale);
+    }
+    double y[K], q[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) y[k] = __fma_rn(y[k], __fma_rn(-t[k], y[k], 1.0), y[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        q[k] = 0.5 * y[k];
+        c[k] = 0.5 * t[k] + __fma_rn(__fma_rn(-t[k], q[k], 0.5), y[k], q[k]);   // 0.5*t + half_recip(t)
+    }
+    return out;
+}
+
+// F at K independent points (one round of K records per lane); every lane of the wave calls it.
+template <int FID, int K>
+__device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab) {
+    if constexpr (FID == F_COSH4) {
+        double c[K];
+        const bool out = cosh_main_k<K>(x, c, tab);
+        if (__builtin_expect(__ballot(out) != 0ull, 0)) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (!cosh_main_range(x[k])) c[k] = cosh_glibc(x[k], tab);
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) f[k] = c[k] * c[k] * c[k] * c[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) f[k] = sin(1.0 / x[k]);
     }
 }
 

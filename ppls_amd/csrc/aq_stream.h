@@ -23,24 +23,32 @@
 // Every decision is the reference's own arithmetic on the same operands, so the interval tree --
 // tasks and accepted counts -- is bit-identical whatever the schedule.
 #pragma once
+#include <type_traits>
+
 #include "aq_device.h"
 
 namespace aq {
 
 constexpr int PT = 512;             // threads per workgroup
 constexpr int NW = PT / 64;         // waves (workers) per workgroup: 8, two per SIMD
-constexpr int WCAP = 256;           // per-wave LDS ring, records (power of two)
-constexpr int PCAP = 2048;          // per-workgroup LDS pool ring, records (power of two)
+constexpr int MAX_ILP = 2;          // records per lane per round, at most (two interleaved evaluations)
+constexpr int RB = 64 * MAX_ILP;    // records per round, at most
+constexpr int WCAP = 384;           // per-wave LDS ring, records: a round pops RB, pushes <= 2*RB
+constexpr int PCAP = 1024;          // per-workgroup LDS pool ring, records (power of two)
 constexpr int LREC = NW * WCAP + PCAP;   // LDS record slots: 4096 x 36 B = 144 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = 512;             // records per HBM queue chunk
 constexpr int S_W = 2;              // 2^S_W seed positions per wave (4..7 dealt)
-constexpr int GIVE_MIN = 96;        // a busy wave feeds the pool for idle siblings only above this depth
+constexpr int GIVE_MIN = 192;       // a busy wave feeds the pool for idle siblings only above this depth
 constexpr int DONATE_MIN = 128;     // pool records needed before a workgroup donates from its pool
 constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr int MAXK = 256;           // max integrals per launch
+constexpr int CCAP = 4096;          // records per wave cellar (private HBM overflow stack, 144 KiB)
+constexpr int REFILL = 192;         // records a wave takes back from its cellar at once
+constexpr int DEFAULT_GSPLIT = 8;   // a multi-integral launch's job = the share of this many waves
+constexpr int DEFAULT_ILP = 1;      // records per lane per round
 
 // Queue control block (HBM ticket queue) and per-integral histogram accumulators. One per async
 // slot; it must be all-zero when a launch starts -- the host zeroes slots lazily in batches.
@@ -77,6 +85,15 @@ struct Chunk {                      // SoA, one queue slot
     unsigned pad[31];
 };
 
+// A wave's private HBM overflow stack: the bottom (oldest, shallowest) records of a full ring go
+// down here without any lock; the wave takes them back when its ring runs dry, before it looks at
+// the shared pool or seeds new work, so the cellar is empty whenever the wave reports idle. Only
+// the owning wave touches it (one CU, one L2), so it stays on-die.
+struct Cellar {
+    double l[CCAP], r[CCAP], fl[CCAP], fr[CCAP];
+    unsigned dt[CCAP];
+};
+
 struct StreamParams {
     const double2* bounds;          // [nprob] {a, b} per integral
     int nprob;
@@ -85,6 +102,8 @@ struct StreamParams {
     int max_depth;
     int shard, nshards;
     int D;                          // seed depth
+    int shares;                     // jobs per integral: job j = share j % shares of integral j / shares
+    int ilp;                        // records per lane per round (1 or 2)
     unsigned epoch;                 // tags queue slots of this launch (ready[s] == epoch)
     unsigned qcap;                  // queue slots
     unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
@@ -92,6 +111,7 @@ struct StreamParams {
     WgPart* parts;                  // [slot * gridDim.x + wg]
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
     Chunk* chunks;
+    Cellar* cellar;                 // [gridDim.x * NW]
     unsigned* ready;
     const ExpEntry* gtab;
 };
@@ -102,8 +122,9 @@ enum : int {
     DG_T_START = 0, DG_T_SEEDED, DG_T_FIRST_LEAD, DG_T_EXIT, DG_ROUNDS, DG_TASKS, DG_CHUNKS_OUT, DG_CHUNKS_IN,
     DG_RECORDS_OUT, DG_T_WAIT, DG_LEADS, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
     DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
-    DG_SEED_CALLS, DG_FLUSHES, DG_MIXED_ROUNDS, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_PAD,
-    DIAG_WORDS = 32
+    DG_SEED_CALLS, DG_FLUSHES, DG_MIXED_ROUNDS, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_CELLAR_IN,
+    DG_CELLAR_OUT, DG_PAD33, DG_PAD34, DG_PAD35, DG_PAD36, DG_PAD37, DG_PAD38, DG_PAD39,
+    DIAG_WORDS = 40
 };
 
 // Shared (LDS) state of one workgroup.
@@ -188,6 +209,9 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     a.tasks = a.leaves = a.maxd = 0;
 }
 
+// Ring slot of monotonic ring index i (WCAP is not a power of two).
+__device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned)WCAP; }
+
 template <int FID, bool HIST, bool DIAG>
 __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     __shared__ double s_l[LREC], s_r[LREC], s_fl[LREC], s_fr[LREC];
@@ -219,8 +243,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const double eps = P.eps;
     const int max_depth = P.max_depth;
     const int D = P.D;
-    const unsigned V = gridDim.x * (unsigned)NW * (unsigned)P.nshards;
-    const unsigned vw = (blockIdx.x * (unsigned)NW + wid) * (unsigned)P.nshards + (unsigned)P.shard;
+    // jobs: job j seeds share j % shares of integral j / shares (integrals in launch order). Wave w
+    // does job w first; later jobs are claimed from a counter, one claim in flight per wave, so the
+    // waves that draw light shares simply take more of them.
+    const unsigned W = gridDim.x * (unsigned)NW;
+    const unsigned w_all = blockIdx.x * (unsigned)NW + wid;
+    const unsigned shares = (unsigned)P.shares;
+    const unsigned total_jobs = (unsigned)P.nprob * shares;
+    const unsigned V = shares * (unsigned)P.nshards;
     const unsigned long long npos_total = 1ull << D;
     const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per wave (<= 8)
     const unsigned npairs = (unsigned)D * nb;
@@ -235,7 +265,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
     Acc acc{0.0, 0u, 0u, 0u};
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
-    int next_prob = 0;            // next integral this wave seeds
+    unsigned ctop = 0;            // records in this wave's cellar (wave-uniform)
+    Cellar* __restrict__ cel = P.cellar + w_all;
+    unsigned job = w_all;         // the job this wave seeds next (wave-uniform)
+    bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
+    unsigned claim = 0;           // lane 0: the prefetched claim
     unsigned err = 0;
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
     bool counted_idle = false;
@@ -252,7 +286,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         unsigned size = top - bot;
 
         if (size == 0) {
-            // ---- out of records: pool first, then the next integral's seeds, else idle / lead
+            // ---- out of records: own cellar, then the pool, then the next job's seeds, else idle / lead
+            if (ctop > 0) {
+                const unsigned k = min(ctop, (unsigned)REFILL), c0 = ctop - k;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's own spills have landed
+                for (unsigned q = lane; q < k; q += 64) {
+                    const unsigned i = c0 + q, j = base + q;
+                    s_l[j] = ld_wt(&cel->l[i]); s_r[j] = ld_wt(&cel->r[i]); s_fl[j] = ld_wt(&cel->fl[i]);
+                    s_fr[j] = ld_wt(&cel->fr[i]); s_dt[j] = ld_wt(&cel->dt[i]);
+                }
+                ctop = c0;
+                bot = 0;
+                top = k;
+                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_IN], (unsigned long long)k); }
+                continue;
+            }
             unsigned long long ci = 0;
             if constexpr (DIAG) ci = clk();
             if (counted_idle) {
@@ -266,6 +314,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     continue;
                 }
             }
+            if (job_pending) {
+                job = __shfl(claim, 0, 64);
+                job_pending = false;
+            }
             unsigned k = 0;
             bool lead = false, seed = false;
             int phase;
@@ -274,15 +326,15 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned avail = S.ptop - S.pbot;
                 phase = S.phase;
                 if (avail > 0) {
-                    k = min(avail, 64u);
+                    k = min(avail, (unsigned)RB);
                     const unsigned pb = S.pbot;
-                    if (lane < k) copy_rec(R, POOL0 + ((pb + lane) & (PCAP - 1)), base + lane);
+                    for (unsigned i = lane; i < k; i += 64) copy_rec(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
                     if (lane == 0) {
                         S.pbot = pb + k;
                         if (counted_idle) S.idle -= 1;
                     }
                     counted_idle = false;
-                } else if (next_prob < P.nprob) {
+                } else if (job < total_jobs) {
                     seed = true;
                 } else {
                     if (!counted_idle) {
@@ -310,10 +362,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
 
             if (seed) {
-                // ---- wave-local seeding of integral `next_prob` (see the file header)
+                // ---- wave-local seeding of job `job` (see the file header)
                 unsigned long long cs = 0;
                 if constexpr (DIAG) cs = clk();
-                const int p = next_prob++;
+                const int p = (int)(job / shares);
+                const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
+                if (lane == 0) claim = W + g_add(&qctl->spare.v, 1u);   // next job: latency hides behind this one
+                job_pending = true;
                 if (p != tag) {
                     flush_acc(P, acc, tag, lane);
                     tag = p;
@@ -561,12 +616,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
 
         // ---- keep the ring from overflowing: move its bottom 64 records to the pool, else to HBM
-        if (size > (unsigned)(WCAP - 64)) {
+        if (size > (unsigned)WCAP - 64u * (unsigned)P.ilp) {
+            if (ctop + 64u <= (unsigned)CCAP) {
+                // the ring's bottom 64 records go down to this wave's cellar (no lock)
+                const unsigned i = ctop + lane, j = base + ring_slot(bot + lane);
+                cel->l[i] = s_l[j]; cel->r[i] = s_r[j]; cel->fl[i] = s_fl[j]; cel->fr[i] = s_fr[j]; cel->dt[i] = s_dt[j];
+                ctop += 64u;
+                bot += 64u;
+                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], 64ull); }
+                continue;
+            }
             wave_lock(&S.lock, lane, lock_spins);
             const unsigned pt = S.ptop;
             const bool fits = (pt - S.pbot) + 64u <= (unsigned)PCAP;
             if (fits) {
-                copy_rec(R, base + ((bot + lane) & (WCAP - 1)), POOL0 + ((pt + lane) & (PCAP - 1)));
+                copy_rec(R, base + ring_slot(bot + lane), POOL0 + ((pt + lane) & (PCAP - 1)));
                 if (lane == 0) S.ptop = pt + 64u;
             }
             wave_unlock(&S.lock, lane);
@@ -581,7 +645,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 slot = __shfl(slot, 0, 64);
                 if (slot < P.qcap) {
                     const unsigned b = bot;
-                    publish_chunk(P, R, slot, 64u, [&](unsigned i) { return base + ((b + i) & (WCAP - 1)); }, lane);
+                    publish_chunk(P, R, slot, 64u, [&](unsigned i) { return base + ring_slot(b + i); }, lane);
                 } else {
                     err |= ERRB_OVERFLOW;   // records dropped: result invalid, error reported
                 }
@@ -593,13 +657,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
         // ---- feed idle sibling waves
         if (size >= (unsigned)GIVE_MIN && S.idle > 0 && S.ptop == S.pbot) {
-            const unsigned k = size / 2u;   // <= 128
+            const unsigned k = size / 2u;   // <= WCAP / 2
             wave_lock(&S.lock, lane, lock_spins);
             const unsigned pt = S.ptop;
             const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
             if (fits) {
                 for (unsigned i = lane; i < k; i += 64)
-                    copy_rec(R, base + ((bot + i) & (WCAP - 1)), POOL0 + ((pt + i) & (PCAP - 1)));
+                    copy_rec(R, base + ring_slot(bot + i), POOL0 + ((pt + i) & (PCAP - 1)));
                 if (lane == 0) S.ptop = pt + k;
             }
             wave_unlock(&S.lock, lane);
@@ -642,7 +706,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         k = size / 2u;   // may be 0: an empty chunk is harmless
                         if (lane == 0) g_add((int*)&qctl->q_tokens.v, (int)k);
                         const unsigned b = bot;
-                        publish_chunk(P, R, slot, k, [&](unsigned i) { return base + ((b + i) & (WCAP - 1)); }, lane);
+                        publish_chunk(P, R, slot, k, [&](unsigned i) { return base + ring_slot(b + i); }, lane);
                         bot += k;
                     }
                     if (lane == 0) spilled += k;
@@ -657,70 +721,88 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
         }
 
-        // ---- one round: pop up to 64 records from the top of this wave's ring
+        // ---- one round: pop up to 64*K records from the top of this wave's ring, K per lane
         unsigned long long c0 = 0, c1 = 0;
         if constexpr (DIAG) c0 = clk();
-        const unsigned n = min(size, 64u);
-        const unsigned b0 = top - n;
-        const bool active = lane < n;
-        double l = 0, r = 0, fl = 0, fr = 0;
-        unsigned dt = 0;
-        if (active) {
-            const unsigned j = base + ((b0 + lane) & (WCAP - 1));
-            l = s_l[j]; r = s_r[j]; fl = s_fl[j]; fr = s_fr[j]; dt = s_dt[j];
-        }
-        const unsigned d = dt & 255u;
-        const int rtag = (int)(dt >> 8);
-        // records of another integral than the accumulators': flush, then follow lane 0's integral;
-        // lanes still of a third integral account for themselves (rare, only after pool/queue moves)
-        bool solo = false;
-        if (__ballot(active && rtag != tag)) {
-            flush_acc(P, acc, tag, lane);
-            tag = __shfl(rtag, 0, 64);
-            solo = active && rtag != tag;
-            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_MIXED_ROUNDS], 1ull); }
-        }
-        bool refine = false;
-        double mid = 0, fmid = 0;
-        if (active) {
-            const Step st = task_step<FID>(l, r, fl, fr, eps, tab);
-            mid = st.mid;
-            fmid = st.fmid;
-            if (HIST) atomicAdd(&P.ctls[P.first_slot + rtag].hist[d], 1ull);
-            const bool leaf = !st.refine;
-            if (st.refine) {
-                if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
-                else refine = true;
-            } else if (HIST) {
-                atomicAdd(&P.ctls[P.first_slot + rtag].hist[AQ_MAX_LEVELS + d], 1ull);
-            }
-            if (!solo) {
-                ++acc.tasks;
-                acc.maxd = max(acc.maxd, d + 1u);
-                if (leaf) {
-                    acc.area += st.larea + st.rarea;  // :199 -> :149
-                    ++acc.leaves;
+        auto do_round = [&](auto kc) -> unsigned {
+            constexpr int K = decltype(kc)::value;
+            const unsigned n = min(size, 64u * K);
+            const unsigned b0 = top - n;
+            double l[K], r[K], fl[K], fr[K];
+            unsigned dt[K];
+            bool act[K], solo[K], refine[K];
+            bool mixed = false;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                act[k] = lane + 64u * k < n;
+                l[k] = 1.0; r[k] = 1.0; fl[k] = 0.0; fr[k] = 0.0; dt[k] = 0;
+                if (act[k]) {
+                    const unsigned j = base + ring_slot(b0 + 64u * k + lane);
+                    l[k] = s_l[j]; r[k] = s_r[j]; fl[k] = s_fl[j]; fr[k] = s_fr[j]; dt[k] = s_dt[j];
                 }
-            } else {
-                WgPart* w = P.parts + (size_t)(P.first_slot + rtag) * gridDim.x + blockIdx.x;
-                atomicAdd(&w->tasks, 1ull);
-                atomicMax(&w->levels, d + 1u);
-                if (leaf) {
-                    atomicAdd(&w->area, st.larea + st.rarea);
-                    atomicAdd(&w->leaves, 1ull);
+                mixed |= act[k] && (int)(dt[k] >> 8) != tag;
+                solo[k] = false;
+                refine[k] = false;
+            }
+            // records of another integral than the accumulators': flush, then follow lane 0's
+            // integral; records still of a third one account for themselves (rare: pool/queue moves)
+            if (__ballot(mixed)) {
+                flush_acc(P, acc, tag, lane);
+                tag = __shfl((int)(dt[0] >> 8), 0, 64);
+#pragma unroll
+                for (int k = 0; k < K; ++k) solo[k] = act[k] && (int)(dt[k] >> 8) != tag;
+                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_MIXED_ROUNDS], 1ull); }
+            }
+            Step st[K];
+            task_step_k<FID, K>(l, r, fl, fr, eps, tab, st);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (!act[k]) continue;
+                const unsigned d = dt[k] & 255u;
+                const int rtag = (int)(dt[k] >> 8);
+                if (HIST) atomicAdd(&P.ctls[P.first_slot + rtag].hist[d], 1ull);
+                const bool leaf = !st[k].refine;
+                if (st[k].refine) {
+                    if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
+                    else refine[k] = true;
+                } else if (HIST) {
+                    atomicAdd(&P.ctls[P.first_slot + rtag].hist[AQ_MAX_LEVELS + d], 1ull);
+                }
+                if (!solo[k]) {
+                    ++acc.tasks;
+                    acc.maxd = max(acc.maxd, d + 1u);
+                    if (leaf) {
+                        acc.area += st[k].larea + st[k].rarea;  // :199 -> :149
+                        ++acc.leaves;
+                    }
+                } else {
+                    WgPart* w = P.parts + (size_t)(P.first_slot + rtag) * gridDim.x + blockIdx.x;
+                    atomicAdd(&w->tasks, 1ull);
+                    atomicMax(&w->levels, d + 1u);
+                    if (leaf) {
+                        atomicAdd(&w->area, st[k].larea + st[k].rarea);
+                        atomicAdd(&w->leaves, 1ull);
+                    }
                 }
             }
-        }
-        if constexpr (DIAG) c1 = clk();
-        const unsigned long long mask = __ballot(refine);
-        if (refine) {
-            const unsigned pos = b0 + 2u * mbcnt(mask);
-            const unsigned j0 = base + (pos & (WCAP - 1)), j1 = base + ((pos + 1u) & (WCAP - 1));
-            const unsigned cdt = (d + 1u) | ((unsigned)rtag << 8);
-            s_l[j0] = l;   s_r[j0] = mid; s_fl[j0] = fl;   s_fr[j0] = fmid; s_dt[j0] = cdt;  // [l,mid]  :192-194
-            s_l[j1] = mid; s_r[j1] = r;   s_fl[j1] = fmid; s_fr[j1] = fr;   s_dt[j1] = cdt;  // [mid,r]  :195-197
-        }
-        top = b0 + 2u * (unsigned)__popcll(mask);
+            if constexpr (DIAG) c1 = clk();
+            unsigned pushed = 0;   // children pairs so far this round
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const unsigned long long mask = __ballot(refine[k]);
+                if (refine[k]) {
+                    const unsigned pos = b0 + 2u * (pushed + mbcnt(mask));
+                    const unsigned j0 = base + ring_slot(pos), j1 = base + ring_slot(pos + 1u);
+                    const unsigned cdt = dt[k] + 1u;   // depth + 1, same integral
+                    s_l[j0] = l[k];      s_r[j0] = st[k].mid; s_fl[j0] = fl[k];      s_fr[j0] = st[k].fmid; s_dt[j0] = cdt;  // :192-194
+                    s_l[j1] = st[k].mid; s_r[j1] = r[k];      s_fl[j1] = st[k].fmid; s_fr[j1] = fr[k];      s_dt[j1] = cdt;  // :195-197
+                }
+                pushed += (unsigned)__popcll(mask);
+            }
+            top = b0 + 2u * pushed;
+            return n;
+        };
+        const unsigned n = P.ilp == 2 ? do_round(std::integral_constant<int, 2>{}) : do_round(std::integral_constant<int, 1>{});
         if constexpr (DIAG) {
             if (lane == 0) {
                 const unsigned long long c2 = clk();

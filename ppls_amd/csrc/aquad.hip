@@ -289,8 +289,11 @@ struct aq_ctx {
     double2* d_bounds = nullptr;       // NSLOTS {a, b}
     double2* h_bounds = nullptr;       // pinned staging, NSLOTS
     Chunk* d_chunks = nullptr;
+    Cellar* d_cellar = nullptr;        // grid * NW per-wave HBM overflow stacks
     unsigned* d_ready = nullptr;
     unsigned epoch = 0;
+    int gsplit_env = 0;                // AQ_GSPLIT: waves per job of a multi-integral launch (0 = default)
+    int ilp_env = 0;                   // AQ_ILP: records per lane per round (0 = default)
     // level path
     DevResults* d_lres = nullptr;
     Rec* d_front[2] = {nullptr, nullptr};
@@ -350,7 +353,14 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.max_depth = max_depth ? max_depth : AQ_DEFAULT_MAX_DEPTH;
     P.shard = shard;
     P.nshards = nshards;
-    P.D = ceil_log2((unsigned long long)G * NW * (unsigned long long)nshards) + S_W;
+    // jobs: one integral is split into one share per wave (the partition the oracle restates); a
+    // multi-integral launch uses gsplit-times larger shares, so one seeding pass feeds more rounds
+    int gs = k >= 16 ? DEFAULT_GSPLIT : 1;
+    if (ctx->gsplit_env > 0) gs = ctx->gsplit_env;
+    while (gs > 1 && (G * NW) % gs != 0) gs >>= 1;
+    P.shares = G * NW / gs;
+    P.ilp = ctx->ilp_env == 1 || ctx->ilp_env == 2 ? ctx->ilp_env : DEFAULT_ILP;
+    P.D = ceil_log2((unsigned long long)P.shares * (unsigned long long)nshards) + S_W;
     P.epoch = ++ctx->epoch;
     if (P.epoch == 0) P.epoch = ++ctx->epoch;
     P.qcap = QCAP;
@@ -359,6 +369,7 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.parts = ctx->d_parts;
     P.diag = ctx->d_diag;
     P.chunks = ctx->d_chunks;
+    P.cellar = ctx->d_cellar;
     P.ready = ctx->d_ready;
     P.gtab = ctx->d_tab;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
@@ -482,6 +493,8 @@ int aq_ctx_create(int device, aq_ctx** out) {
     // One workgroup per CU (the LDS rings take most of a CU's LDS); the whole grid must be
     // resident, because idle workgroups wait on the queue for busy ones.
     c->grid = std::min(c->num_cus, MAXG);
+    if (const char* e = getenv("AQ_GSPLIT")) c->gsplit_env = atoi(e);
+    if (const char* e = getenv("AQ_ILP")) c->ilp_env = atoi(e);
     AQ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     AQ_HIP(hipMalloc(&c->d_tab, sizeof(ExpEntry) * 128));
     AQ_HIP(hipMemcpy(c->d_tab, aq_exp_tab_host, sizeof(ExpEntry) * 128, hipMemcpyHostToDevice));
@@ -492,6 +505,7 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipMalloc(&c->d_bounds, sizeof(double2) * NSLOTS));
     AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS, hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_chunks, sizeof(Chunk) * (size_t)QCAP));
+    AQ_HIP(hipMalloc(&c->d_cellar, sizeof(Cellar) * (size_t)c->grid * NW));
     AQ_HIP(hipMalloc(&c->d_ready, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
     AQ_HIP(hipMemset(c->d_ready, 0, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
     AQ_HIP(hipHostMalloc(&c->h_parts, sizeof(WgPart) * (size_t)c->grid, hipHostMallocDefault));
@@ -515,6 +529,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_parts);
     (void)hipFree(c->d_bounds);
     (void)hipFree(c->d_chunks);
+    (void)hipFree(c->d_cellar);
     (void)hipFree(c->d_ready);
     (void)hipFree(c->d_lres);
     (void)hipFree(c->d_diag);

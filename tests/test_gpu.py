@@ -223,3 +223,26 @@ def test_many_sharded(ctx, oracle, trees):
         tot_t += rs[0].tasks
         tot_l += rs[0].accepted
     assert (tot_t, tot_l) == (g["tasks"], g["leaves"])
+
+
+def test_large_jobs_and_cellar(trees, monkeypatch):
+    """Jobs of 8 waves' shares (deep per-wave subtrees, claimed dynamically): ring overflow goes
+    through the per-wave HBM cellars and every integral still matches the golden tree."""
+    from ppls_amd import Context
+    monkeypatch.setenv("AQ_GSPLIT", "8")
+    c = Context(0)
+    try:
+        c.set_level_histograms(False)
+        c.set_diagnostics(True)
+        g = trees["cosh4_eps1e-12"]
+        k = 32
+        c.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-12, first_slot=0)
+        d, f = c.diagnostics()
+        for i in range(k):
+            r = c.fetch(i)
+            assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"])
+            assert _area_ok(r.area, g["area_quad"])
+        col = dict(zip(f, d.T))
+        assert col["cellar_out"].sum() > 0 and col["cellar_out"].sum() == col["cellar_in"].sum()
+    finally:
+        c.close()

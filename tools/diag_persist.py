@@ -36,7 +36,7 @@ def summarize(d, f):
     s["cyc_seed_per_wg_p50"] = float(np.median(col["c_seed"]))
     s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
                   "sum": col["tasks"].sum()}
-    for k in ("leads", "pool_push", "pool_take", "give", "lock_spins", "spill_records", "chunks_out", "chunks_in",
+    for k in ("leads", "pool_push", "pool_take", "give", "cellar_in", "cellar_out", "lock_spins", "spill_records", "chunks_out", "chunks_in",
               "records_out", "records_in", "seed_calls", "mixed_rounds"):
         s[k] = {"sum": col[k].sum(), "max": col[k].max()}
     s["t_wait_us_p50"] = float(np.median(col["t_wait"])) / 100.0
