@@ -66,8 +66,11 @@ int aq_device_count(int *count);
 int aq_ctx_create(int device, aq_ctx **out);
 void aq_ctx_destroy(aq_ctx *ctx);
 const char *aq_strerror(int code);
-/* Compute units of the context's device (the "workers" of the on-device farmer). */
+/* Compute units of the context's device (one persistent workgroup each). */
 int aq_ctx_num_cus(const aq_ctx *ctx);
+/* Wavefront workers of the on-device farmer (workgroups x waves per workgroup): one integral
+ * launched alone is split into this many shares (the partition aq_integrate_shard documents). */
+int aq_ctx_num_workers(const aq_ctx *ctx);
 /* Per-level task/accepted histograms on the persistent path (default on; a diagnostic the
  * reference does not produce -- pipelined callers switch it off). */
 int aq_set_level_histograms(aq_ctx *ctx, int enable);
@@ -80,10 +83,12 @@ int aq_set_level_histograms(aq_ctx *ctx, int enable);
  */
 int aq_integrate(aq_ctx *ctx, const aq_problem *p, aq_result *res);
 
-/* This process's share of a multi-GPU run: the depth-D frontier is dealt cyclically over
- * nshards*workgroups virtual workers; shard `shard` evaluates its subtrees plus the tasks
- * above depth D it owns (each counted by exactly one shard). Summing area/tasks/accepted over
- * all shards (the caller's all-reduce) gives exactly the single-GPU result. */
+/* This process's share of a multi-GPU run: the depth-D positions (D = ceil(log2(V)) + 2) are
+ * dealt in snake order over V = nshards * aq_ctx_num_workers() virtual workers; shard `shard`
+ * evaluates its positions' subtrees plus the tasks at depth <= D it owns (each counted by the
+ * owner of its leftmost descendant position, so by exactly one shard). Summing
+ * area/tasks/accepted over all shards (the caller's all-reduce) gives exactly the single-GPU
+ * result. */
 int aq_integrate_shard(aq_ctx *ctx, const aq_problem *p, int shard, int nshards, aq_result *res);
 
 /* Asynchronous form for pipelined callers (bench): enqueue one integral on the context's stream,

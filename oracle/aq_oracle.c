@@ -289,8 +289,8 @@ int aqo_integrate(int integrand, int mode, double a, double b, double eps, int m
 }
 
 /*
- * The share of shard `shard` of `nshards` in the device's partition (ppls_amd/csrc/aquad.hip,
- * k_persist seeding): V = G*nshards virtual workers, seed depth D = ceil(log2 V) + S; virtual
+ * The share of shard `shard` of `nshards` in the device's partition (ppls_amd/csrc/aq_stream.h,
+ * k_stream seeding): V = G*nshards virtual workers, seed depth D = floor(log2 V) + S; virtual
  * worker vwg = w*nshards + shard owns the depth-D positions j = k*V + (k odd ? V-1-vwg : vwg) < 2^D;
  * a task above depth D is counted by the owner of its leftmost descendant position. Summing the
  * results of all shards gives aqo_integrate()'s counts exactly (tests check both properties).
@@ -307,7 +307,7 @@ int aqo_integrate_shard(int integrand, int mode, double a, double b, double eps,
     if (leaves_per_level) memset(leaves_per_level, 0, sizeof(uint64_t) * (size_t)maxlev);
     const uint64_t V = (uint64_t)G * (uint64_t)nshards;
     int D = 0;
-    while ((1ull << D) < V) D++;
+    while ((2ull << D) <= V) D++;
     D += S;
     const uint64_t npos = 1ull << D;
     const uint64_t nbands = (npos + V - 1) / V;

@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(HERE, "_build", "libaquad.so")
 
 # Every symbol include/aquad.h declares (tests check the library exports all of them).
 EXPORTS = (
-    "aq_device_count", "aq_ctx_create", "aq_ctx_destroy", "aq_strerror", "aq_ctx_num_cus",
+    "aq_device_count", "aq_ctx_create", "aq_ctx_destroy", "aq_strerror", "aq_ctx_num_cus", "aq_ctx_num_workers",
     "aq_set_level_histograms",
     "aq_integrate", "aq_integrate_shard", "aq_async_slots", "aq_integrate_async", "aq_fetch",
     "aq_max_integrals_per_launch", "aq_integrate_many_async",
@@ -58,6 +58,7 @@ def load(build_if_missing=True):
         "aq_ctx_destroy": ([vp], None),
         "aq_strerror": ([ctypes.c_int], ctypes.c_char_p),
         "aq_ctx_num_cus": ([vp], ctypes.c_int),
+        "aq_ctx_num_workers": ([vp], ctypes.c_int),
         "aq_set_level_histograms": ([vp, ctypes.c_int], ctypes.c_int),
         "aq_integrate": ([vp, P, R], ctypes.c_int),
         "aq_integrate_shard": ([vp, P, ctypes.c_int, ctypes.c_int, R], ctypes.c_int),

@@ -88,6 +88,7 @@ class Context:
         _check(self.L.aq_ctx_create(int(device), ctypes.byref(self._h)), "aq_ctx_create")
         self.device = device
         self.num_cus = self.L.aq_ctx_num_cus(self._h)
+        self.num_workers = self.L.aq_ctx_num_workers(self._h)
 
     def close(self):
         if self._h:
@@ -189,7 +190,7 @@ class Context:
                    "records_out", "t_wait", "leads", "seeds", "pool_push", "cu", "records_in", "active_lanes",
                    "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed",
                    "seed_calls", "c_seed_resolve", "mixed_rounds", "c_idle", "c_seed_pass1", "c_seed_pass2", "give", "cellar_in",
-                   "cellar_out", "pad33", "pad34", "pad35", "pad36", "pad37", "pad38", "pad39")
+                   "cellar_out", "c_refill", "c_loop", "active_tasks", "prefetch", "pad37", "pad38", "pad39")
     DIAG_WORDS = 40
 
     def set_diagnostics(self, enable: bool):

@@ -85,6 +85,36 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
     }
 }
 
+// Double-double (hi + lo) sums of the accepted areas: every leaf area enters a per-lane pair
+// exactly (Knuth's TwoSum, six flops), the pairs reduce across the wave and the workers without
+// rounding, and only the final hi + lo is rounded -- so the area is the correctly rounded sum of
+// the leaf areas whatever the schedule (the order-dependent double sum of the farmer's
+// `result += buff[0]`, :149, is within a few ulps of it).
+__host__ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+    s = a + b;
+    const double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+__host__ __device__ __forceinline__ void dd_add(double& hi, double& lo, double v) {
+    double s, e;
+    two_sum(hi, v, s, e);
+    hi = s;
+    lo += e;
+}
+__host__ __device__ __forceinline__ void dd_add_dd(double& hi, double& lo, double h2, double l2) {
+    double s, e;
+    two_sum(hi, h2, s, e);
+    e += lo + l2;
+    two_sum(s, e, hi, lo);
+}
+__device__ __forceinline__ void wave_sum_dd(double& hi, double& lo) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double h2 = __shfl_xor(hi, o, 64), l2 = __shfl_xor(lo, o, 64);
+        dd_add_dd(hi, lo, h2, l2);
+    }
+}
+
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
 
 __device__ __forceinline__ unsigned long long clk() {

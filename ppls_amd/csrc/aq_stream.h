@@ -2,58 +2,61 @@
 //
 // Reference: /root/reference/aquadPartA.c. The farmer's LIFO bag (:125-173) and the workers' task
 // body (:183-202) become one persistent launch:
-//   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of interval records
-//     {l, r, F(l), F(r), depth | integral<<8}. A round pops <= 64 records, evaluates F(mid) for each
-//     in FP64 (glibc-exact cosh, aq_libm.h), applies the reference's refine test (:191) and pushes the
-//     children (:192-197) back with a ballot / mbcnt compaction: no workgroup barrier, no HBM traffic.
-//   * work sharing inside a CU: a locked LDS pool (ring overflow in, idle waves out);
-//   * work sharing across CUs (what the bag of tasks is for): an HBM ticket queue of record chunks,
-//     driven by one elected leader wave per workgroup; busy waves donate to waiting tickets;
-//   * seeding is WAVE-LOCAL: virtual worker vw = ((wg*NW + wave)*nshards + shard) of V owns the
-//     depth-D positions j = k*V + (k odd ? V-1-vw : vw) (snake order). All F evaluations of the
-//     positions' ancestors are independent (pure (l+r)/2 recursion), so one wave evaluates them in one
-//     pass, decides every ancestor in a second pass and keeps the surviving positions as its first
-//     records. A task above depth D is counted by the owner of its leftmost descendant position.
-//   * a wave that runs out of records takes from the pool, else seeds its share of the NEXT
-//     integral of the launch -- the tail of one integral overlaps the start of the next, which is
-//     what keeps all lanes busy (a single integral's frontier is too narrow to fill a CU).
+//   * the unit of work is a SIBLING PAIR {a, m, b, F(a), F(m), F(b), depth | integral<<8}
+//     = the two tasks [a,m] and [m,b] a refining parent pushes (:192-197). A pair is 52 bytes for two
+//     tasks (two separate records would be 72), and it hands every lane two independent
+//     evaluations: the K=2 cosh chains interleave (aq_libm.h cosh_main_k).
+//   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of pairs. A round pops
+//     <= 64 pairs, evaluates F at both midpoints in FP64 (glibc-exact cosh), applies the reference's
+//     refine test (:191) to both tasks and pushes each refining task's children as a new pair, with a
+//     ballot / mbcnt compaction: no workgroup barrier, no HBM traffic.
+//   * ring overflow goes to the wave's private HBM cellar (no lock; refilled when the ring runs dry);
+//     a locked LDS pool feeds idle sibling waves; an HBM ticket queue of pair chunks moves work
+//     across CUs (what the bag of tasks is for), driven by one elected leader wave per idle
+//     workgroup; busy waves donate to waiting tickets.
+//   * jobs: job j seeds share j % shares of integral j / shares. Seeding is WAVE-LOCAL: virtual
+//     worker vw = share*nshards + shard of V owns the depth-D positions j = k*V + (k odd ? V-1-vw : vw)
+//     (snake order). All F evaluations of the positions' paths (depths 0..D) are independent (pure
+//     (l+r)/2 recursion), so one wave evaluates them in one pass, decides every node, and keeps the
+//     children of each surviving position node as its first pair. A task at depth <= D is counted by
+//     the owner of its leftmost descendant position (the partition oracle/aq_oracle.c restates).
+//     Wave w seeds job w first; later jobs are claimed from a counter (one claim in flight per wave),
+//     so the tail of one integral overlaps the start of the next, and waves that draw light shares
+//     take more of them.
 //   * accepted areas / task counts accumulate per lane in registers per integral and are flushed
 //     (wave reduction + one set of uncontended atomics into this workgroup's partial of that
 //     integral) when a wave switches integral or exits (the farmer's `result += buff[0]`, :149).
 // Every decision is the reference's own arithmetic on the same operands, so the interval tree --
 // tasks and accepted counts -- is bit-identical whatever the schedule.
 #pragma once
-#include <type_traits>
-
 #include "aq_device.h"
 
 namespace aq {
 
-constexpr int PT = 512;             // threads per workgroup
-constexpr int NW = PT / 64;         // waves (workers) per workgroup: 8, two per SIMD
-constexpr int MAX_ILP = 2;          // records per lane per round, at most (two interleaved evaluations)
-constexpr int RB = 64 * MAX_ILP;    // records per round, at most
-constexpr int WCAP = 384;           // per-wave LDS ring, records: a round pops RB, pushes <= 2*RB
-constexpr int PCAP = 1024;          // per-workgroup LDS pool ring, records (power of two)
-constexpr int LREC = NW * WCAP + PCAP;   // LDS record slots: 4096 x 36 B = 144 KiB
+constexpr int PT = 768;             // threads per workgroup
+constexpr int NW = PT / 64;         // waves (workers) per workgroup: 12, three per SIMD
+constexpr int WCAP = 208;           // per-wave LDS ring, pairs: a round pops <= 64, pushes <= 128
+constexpr int PCAP = 256;           // per-workgroup LDS pool ring, pairs (power of two)
+constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 2752 x 52 B = 140 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
-constexpr int CH = 512;             // records per HBM queue chunk
-constexpr int S_W = 2;              // 2^S_W seed positions per wave (4..7 dealt)
-constexpr int GIVE_MIN = 192;       // a busy wave feeds the pool for idle siblings only above this depth
-constexpr int DONATE_MIN = 128;     // pool records needed before a workgroup donates from its pool
+constexpr int CH = 256;             // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
+constexpr int S_W = 2;              // seed depth D = floor(log2 V) + S_W: 3 or 4 positions per share
+constexpr int GIVE_MIN = 96;        // a busy wave feeds the pool for idle siblings only above this size
+constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup donates from its pool
 constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
+constexpr int GIVE_ROUNDS = 4;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr int MAXK = 256;           // max integrals per launch
-constexpr int CCAP = 4096;          // records per wave cellar (private HBM overflow stack, 144 KiB)
-constexpr int REFILL = 192;         // records a wave takes back from its cellar at once
-constexpr int DEFAULT_GSPLIT = 8;   // a multi-integral launch's job = the share of this many waves
-constexpr int DEFAULT_ILP = 1;      // records per lane per round
+constexpr int DEFAULT_GSPLIT = 16;  // a multi-integral launch's job = the share of this many waves
+constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
+constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
+constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches 64 cellar pairs
 
 // Queue control block (HBM ticket queue) and per-integral histogram accumulators. One per async
 // slot; it must be all-zero when a launch starts -- the host zeroes slots lazily in batches.
 // q_tokens stores (tokens - G): the protocol's token count starts at G (every workgroup busy) and
-// the run is over when it reaches 0.
+// the run is over when it reaches 0. jobs counts claimed jobs beyond the first W.
 struct alignas(128) Line {
     unsigned v;
     unsigned pad[31];
@@ -62,35 +65,36 @@ struct Ctl {
     Line q_tail;               // chunk slots claimed by producers
     Line q_head;               // tickets taken by idle workgroups
     Line q_tokens;             // tokens - G
-    Line spare;
+    Line jobs;                 // job claims
     unsigned long long hist[2 * AQ_MAX_LEVELS];   // [0,L): tasks per level, [L,2L): accepted per level
 };
 
 // One workgroup's share of one integral, accumulated with uncontended atomics (zeroed per slot).
+// Its area lives in the per-wave double-double partials (StreamParams::warea), not here.
 struct WgPart {
-    double area;
+    unsigned long long spare;
     unsigned long long tasks;
     unsigned long long leaves;
-    unsigned long long spilled;
+    unsigned long long spilled;   // pairs this workgroup moved through the HBM queue (slot first_slot)
     unsigned levels;
     unsigned error;
-    unsigned cu;               // hardware CU slot
+    unsigned cu;                  // hardware CU slot
     unsigned pad;
 };
 
 struct Chunk {                      // SoA, one queue slot
-    double l[CH], r[CH], fl[CH], fr[CH];
-    unsigned dt[CH];                // depth | integral << 8
+    double a[CH], m[CH], b[CH], fa[CH], fm[CH], fb[CH];
+    unsigned dt[CH];
     unsigned count;
     unsigned pad[31];
 };
 
-// A wave's private HBM overflow stack: the bottom (oldest, shallowest) records of a full ring go
+// A wave's private HBM overflow stack: the bottom (oldest, shallowest) pairs of a full ring go
 // down here without any lock; the wave takes them back when its ring runs dry, before it looks at
 // the shared pool or seeds new work, so the cellar is empty whenever the wave reports idle. Only
 // the owning wave touches it (one CU, one L2), so it stays on-die.
 struct Cellar {
-    double l[CCAP], r[CCAP], fl[CCAP], fr[CCAP];
+    double a[CCAP], m[CCAP], b[CCAP], fa[CCAP], fm[CCAP], fb[CCAP];
     unsigned dt[CCAP];
 };
 
@@ -101,14 +105,14 @@ struct StreamParams {
     double eps;
     int max_depth;
     int shard, nshards;
-    int D;                          // seed depth
+    int D;                          // seed position depth
     int shares;                     // jobs per integral: job j = share j % shares of integral j / shares
-    int ilp;                        // records per lane per round (1 or 2)
     unsigned epoch;                 // tags queue slots of this launch (ready[s] == epoch)
     unsigned qcap;                  // queue slots
     unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
     Ctl* ctls;                      // per-slot control blocks; the queue uses ctls[first_slot]
     WgPart* parts;                  // [slot * gridDim.x + wg]
+    double2* warea;                 // [slot * gridDim.x * NW + wave]: {hi, lo} area of that wave's leaves
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
     Chunk* chunks;
     Cellar* cellar;                 // [gridDim.x * NW]
@@ -123,7 +127,7 @@ enum : int {
     DG_RECORDS_OUT, DG_T_WAIT, DG_LEADS, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
     DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
     DG_SEED_CALLS, DG_FLUSHES, DG_MIXED_ROUNDS, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_CELLAR_IN,
-    DG_CELLAR_OUT, DG_PAD33, DG_PAD34, DG_PAD35, DG_PAD36, DG_PAD37, DG_PAD38, DG_PAD39,
+    DG_CELLAR_OUT, DG_C_REFILL, DG_C_LOOP, DG_ACTIVE_TASKS, DG_PREFETCH, DG_PAD37, DG_PAD38, DG_PAD39,
     DIAG_WORDS = 40
 };
 
@@ -131,18 +135,20 @@ enum : int {
 struct WgState {
     int lock;            // pool lock (lane 0 of the holding wave)
     unsigned pbot, ptop; // pool ring, monotonic indices
-    int idle;            // waves with nothing left (no records, pool empty, nothing to seed)
+    int idle;            // waves with nothing left (no pairs, pool empty, nothing to seed)
     int phase;           // 0 running, 1 a leader wave is at the HBM queue, 2 exit
     int busy_token;      // the workgroup holds one token of the HBM-queue protocol
     int pad[2];
 };
 
-// LDS record arrays (SoA), one per field.
-struct LdsRecs {
-    double* l;
-    double* r;
-    double* fl;
-    double* fr;
+// LDS pair arrays (SoA), one per field.
+struct LdsPairs {
+    double* a;
+    double* m;
+    double* b;
+    double* fa;
+    double* fm;
+    double* fb;
     unsigned* dt;
 };
 
@@ -166,21 +172,22 @@ __device__ __forceinline__ void wave_unlock(int* lock, unsigned lane) {
     if (lane == 0) __hip_atomic_store(lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__device__ __forceinline__ void copy_rec(const LdsRecs& R, unsigned i, unsigned j) {
-    const double l = R.l[i], r = R.r[i], fl = R.fl[i], fr = R.fr[i];
+__device__ __forceinline__ void copy_pair(const LdsPairs& R, unsigned i, unsigned j) {
+    const double a = R.a[i], m = R.m[i], b = R.b[i], fa = R.fa[i], fm = R.fm[i], fb = R.fb[i];
     const unsigned dt = R.dt[i];
-    R.l[j] = l; R.r[j] = r; R.fl[j] = fl; R.fr[j] = fr; R.dt[j] = dt;
+    R.a[j] = a; R.m[j] = m; R.b[j] = b; R.fa[j] = fa; R.fm[j] = fm; R.fb[j] = fb; R.dt[j] = dt;
 }
 
-// Publish k records (LDS slots src(i), i < k) as HBM chunk `slot` (caller: one whole wave).
+// Publish k pairs (LDS slots src(i), i < k) as HBM chunk `slot` (caller: one whole wave).
 template <typename SrcIdx>
-__device__ __forceinline__ void publish_chunk(const StreamParams& P, const LdsRecs& R, unsigned slot, unsigned k,
+__device__ __forceinline__ void publish_chunk(const StreamParams& P, const LdsPairs& R, unsigned slot, unsigned k,
                                               SrcIdx src, unsigned lane) {
     Chunk* __restrict__ c = P.chunks + slot;
     for (unsigned i = lane; i < k; i += 64) {
         const unsigned j = src(i);
-        st_wt(&c->l[i], R.l[j]); st_wt(&c->r[i], R.r[j]); st_wt(&c->fl[i], R.fl[j]);
-        st_wt(&c->fr[i], R.fr[j]); st_wt(&c->dt[i], R.dt[j]);
+        st_wt(&c->a[i], R.a[j]); st_wt(&c->m[i], R.m[j]); st_wt(&c->b[i], R.b[j]);
+        st_wt(&c->fa[i], R.fa[j]); st_wt(&c->fm[i], R.fm[j]); st_wt(&c->fb[i], R.fb[j]);
+        st_wt(&c->dt[i], R.dt[j]);
     }
     if (lane == 0) st_wt(&c->count, k);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the single storing wave drains
@@ -189,23 +196,30 @@ __device__ __forceinline__ void publish_chunk(const StreamParams& P, const LdsRe
 
 // Per-wave accumulators of the integral currently being summed (`tag`).
 struct Acc {
-    double area;
+    double hi, lo;                  // double-double area (aq_device.h two_sum)
     unsigned tasks, leaves, maxd;
 };
 
-// Flush a wave's accumulators for integral `tag` into this workgroup's partial (one lane, three
-// to five uncontended atomics), and reset them.
-__device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane) {
-    const double s = wave_sum(a.area);
+// Flush a wave's accumulators for integral `tag`: counts into this workgroup's partial (three
+// uncontended integer atomics), the double-double area into the wave's own partial (a plain
+// read-modify-write: no other wave touches it), and reset them.
+__device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all) {
+    double hi = a.hi, lo = a.lo;
+    wave_sum_dd(hi, lo);
     const unsigned t = wave_sum_u(a.tasks), l = wave_sum_u(a.leaves), m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
         WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
-        atomicAdd(&w->area, s);
         atomicAdd(&w->tasks, (unsigned long long)t);
         atomicAdd(&w->leaves, (unsigned long long)l);
         atomicMax(&w->levels, m);
+        double* q = &P.warea[(size_t)(P.first_slot + tag) * gridDim.x * NW + w_all].x;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
+        double h0 = ld_wt(q), l0 = ld_wt(q + 1);
+        dd_add_dd(h0, l0, hi, lo);
+        st_wt(q, h0);
+        st_wt(q + 1, l0);
     }
-    a.area = 0.0;
+    a.hi = a.lo = 0.0;
     a.tasks = a.leaves = a.maxd = 0;
 }
 
@@ -214,7 +228,7 @@ __device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned
 
 template <int FID, bool HIST, bool DIAG>
 __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
-    __shared__ double s_l[LREC], s_r[LREC], s_fl[LREC], s_fr[LREC];
+    __shared__ double s_a[LREC], s_m[LREC], s_b[LREC], s_fa[LREC], s_fm[LREC], s_fb[LREC];
     __shared__ unsigned s_dt[LREC];
     __shared__ ExpEntry tab[128];
     __shared__ WgState S;
@@ -225,7 +239,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const unsigned lane = lane_id();
     const unsigned wid = tid >> 6;
     Ctl* __restrict__ qctl = P.ctls + P.first_slot;
-    const LdsRecs R{s_l, s_r, s_fl, s_fr, s_dt};
+    const LdsPairs R{s_a, s_m, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned long long t_entry = rtc();
     stage_exp_table(tab, P.gtab);
     if (tid == 0) {
@@ -243,29 +257,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const double eps = P.eps;
     const int max_depth = P.max_depth;
     const int D = P.D;
-    // jobs: job j seeds share j % shares of integral j / shares (integrals in launch order). Wave w
-    // does job w first; later jobs are claimed from a counter, one claim in flight per wave, so the
-    // waves that draw light shares simply take more of them.
     const unsigned W = gridDim.x * (unsigned)NW;
     const unsigned w_all = blockIdx.x * (unsigned)NW + wid;
     const unsigned shares = (unsigned)P.shares;
     const unsigned total_jobs = (unsigned)P.nprob * shares;
     const unsigned V = shares * (unsigned)P.nshards;
     const unsigned long long npos_total = 1ull << D;
-    const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per wave (<= 8)
-    const unsigned npairs = (unsigned)D * nb;
+    const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per share (<= 8)
+    const unsigned nlev = (unsigned)D + 1u;                     // seeding evaluates depths 0..D
+    const unsigned nnodes = nlev * nb;
     const unsigned base = wid * WCAP;                            // this wave's ring
-    // seeding fast path (npairs <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
+    // seeding fast path (nnodes <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
     unsigned long long colmask = 0;
-    if (npairs <= 64) {
+    if (nnodes <= 64) {
         const unsigned kk = lane % nb;
-        for (int d = 0; d < D; ++d)
-            if ((unsigned)d * nb + kk < 64u) colmask |= 1ull << ((unsigned)d * nb + kk);
+        for (unsigned d = 0; d < nlev; ++d)
+            if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
     }
 
-    Acc acc{0.0, 0u, 0u, 0u};
+    Acc acc{0.0, 0.0, 0u, 0u, 0u};
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
-    unsigned ctop = 0;            // records in this wave's cellar (wave-uniform)
+    unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
     Cellar* __restrict__ cel = P.cellar + w_all;
     unsigned job = w_all;         // the job this wave seeds next (wave-uniform)
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
@@ -275,30 +287,58 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     bool counted_idle = false;
     unsigned poll_ctr = wid * (POLL_ROUNDS / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
-    unsigned long long spilled = 0;          // records this wave sent to HBM (lane 0)
+    unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
     unsigned long long lock_spins = 0;
+    // cellar prefetch in flight: up to 64 pairs, one per lane, landed below the ring's bottom at
+    // the top of the next iteration (the loads overlap one round)
+    unsigned pf_n = 0;
+    double pf_a = 0, pf_m = 0, pf_b = 0, pf_fa = 0, pf_fm = 0, pf_fb = 0;
+    unsigned pf_dt = 0;
     const unsigned long long t0 = rtc();
+    unsigned long long cl0 = 0;
     if constexpr (DIAG) {
         if (tid == 0) s_dg[DG_T_START] = t_entry;
+        cl0 = clk();
     }
 
     for (;;) {
+        if (pf_n) {
+            if (bot < 64u) {   // keep ring indices non-negative (slots are index % WCAP)
+                bot += (unsigned)WCAP;
+                top += (unsigned)WCAP;
+            }
+            bot -= pf_n;
+            if (lane < pf_n) {
+                const unsigned j = base + ring_slot(bot + lane);
+                s_a[j] = pf_a; s_m[j] = pf_m; s_b[j] = pf_b; s_fa[j] = pf_fa; s_fm[j] = pf_fm; s_fb[j] = pf_fb;
+                s_dt[j] = pf_dt;
+            }
+            pf_n = 0;
+        }
         unsigned size = top - bot;
 
         if (size == 0) {
-            // ---- out of records: own cellar, then the pool, then the next job's seeds, else idle / lead
+            // ---- out of pairs: own cellar, then the pool, then the next job's seeds, else idle / lead
             if (ctop > 0) {
+                unsigned long long cr = 0;
+                if constexpr (DIAG) cr = clk();
                 const unsigned k = min(ctop, (unsigned)REFILL), c0 = ctop - k;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's own spills have landed
                 for (unsigned q = lane; q < k; q += 64) {
                     const unsigned i = c0 + q, j = base + q;
-                    s_l[j] = ld_wt(&cel->l[i]); s_r[j] = ld_wt(&cel->r[i]); s_fl[j] = ld_wt(&cel->fl[i]);
-                    s_fr[j] = ld_wt(&cel->fr[i]); s_dt[j] = ld_wt(&cel->dt[i]);
+                    s_a[j] = ld_wt(&cel->a[i]); s_m[j] = ld_wt(&cel->m[i]); s_b[j] = ld_wt(&cel->b[i]);
+                    s_fa[j] = ld_wt(&cel->fa[i]); s_fm[j] = ld_wt(&cel->fm[i]); s_fb[j] = ld_wt(&cel->fb[i]);
+                    s_dt[j] = ld_wt(&cel->dt[i]);
                 }
                 ctop = c0;
                 bot = 0;
                 top = k;
-                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_IN], (unsigned long long)k); }
+                if constexpr (DIAG) {
+                    if (lane == 0) {
+                        atomicAdd(&s_dg[DG_CELLAR_IN], (unsigned long long)k);
+                        atomicAdd(&s_dg[DG_C_REFILL], clk() - cr);
+                    }
+                }
                 continue;
             }
             unsigned long long ci = 0;
@@ -326,9 +366,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned avail = S.ptop - S.pbot;
                 phase = S.phase;
                 if (avail > 0) {
-                    k = min(avail, (unsigned)RB);
+                    k = min(avail, (unsigned)REFILL);
                     const unsigned pb = S.pbot;
-                    for (unsigned i = lane; i < k; i += 64) copy_rec(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
+                    for (unsigned i = lane; i < k; i += 64) copy_pair(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
                     if (lane == 0) {
                         S.pbot = pb + k;
                         if (counted_idle) S.idle -= 1;
@@ -367,17 +407,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if constexpr (DIAG) cs = clk();
                 const int p = (int)(job / shares);
                 const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
-                if (lane == 0) claim = W + g_add(&qctl->spare.v, 1u);   // next job: latency hides behind this one
+                if (lane == 0) claim = W + g_add(&qctl->jobs.v, 1u);   // next job: latency hides behind this one
                 job_pending = true;
                 if (p != tag) {
-                    flush_acc(P, acc, tag, lane);
+                    flush_acc(P, acc, tag, lane, w_all);
                     tag = p;
                 }
                 const double2 ab = s_bounds[p];
                 const double A = ab.x, B = ab.y;
-                double* fm = s_l + base;          // [npairs + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
-                double* leafa = s_r + base;       // [npairs]: larea + rarea of node (d,k)
-                unsigned* flag = s_dt + base;     // [npairs]: node (d,k) refines
+                double* fm = s_a + base;          // [nnodes + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
+                double* leafa = s_m + base;       // [nnodes]: larea + rarea of node (d,k)
+                unsigned* flag = s_dt + base;     // [nnodes]: node (d,k) refines
                 auto position = [&](unsigned kk, bool& valid) -> unsigned long long {
                     const unsigned long long o = (kk & 1u) ? (unsigned long long)(V - 1 - vw) : (unsigned long long)vw;
                     const unsigned long long j = (unsigned long long)kk * V + o;
@@ -386,28 +426,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 };
                 unsigned long long cp1 = 0, cp2 = 0;
                 bool alive = false;
-                double l = A, r = B, fl = 0.0, fr = 0.0;
-                if (npairs <= 64) {
+                double l = A, r = B, fl = 0.0, fr = 0.0, mid = 0.0, fmid = 0.0;
+                if (nnodes <= 64) {
                     // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
                     // decision; the first leaf depth of every position comes from ONE ballot
                     const unsigned q = lane;
-                    const bool isnode = q < npairs;
+                    const bool isnode = q < nnodes;
                     const unsigned d = isnode ? q / nb : 0u, kk = isnode ? q - d * nb : 0u;
                     bool valid = false;
                     const unsigned long long pp = isnode ? position(kk, valid) : 0ull;
                     const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
-                    unsigned li = npairs, ri = npairs + 1;
+                    unsigned li = nnodes, ri = nnodes + 1;
                     for (unsigned i = 0; i < d; ++i) {
-                        const double m = (l + r) / 2;
-                        if ((anc >> (d - 1 - i)) & 1ull) { l = m; li = i * nb + kk; } else { r = m; ri = i * nb + kk; }
+                        const double mm = (l + r) / 2;
+                        if ((anc >> (d - 1 - i)) & 1ull) { l = mm; li = i * nb + kk; } else { r = mm; ri = i * nb + kk; }
                     }
-                    const double mid = (l + r) / 2;                           // :187
-                    const unsigned fq = npairs + 2 <= 64 ? q : (q < npairs ? q : 64u);
-                    double fmid = 0.0;
-                    if (fq < npairs + 2)
-                        fmid = integrand<FID>(isnode ? mid : (q == npairs ? A : B), tab);   // :188
-                    if (fq < npairs + 2) fm[q] = fmid;
-                    if (npairs + 2 > 64 && lane < 2) fm[npairs + lane] = integrand<FID>(lane == 0 ? A : B, tab);
+                    mid = (l + r) / 2;                                        // :187
+                    const unsigned fq = nnodes + 2 <= 64 ? q : (q < nnodes ? q : 64u);
+                    if (fq < nnodes + 2)
+                        fmid = integrand<FID>(isnode ? mid : (q == nnodes ? A : B), tab);   // :188
+                    if (fq < nnodes + 2) fm[q] = fmid;
+                    if (nnodes + 2 > 64 && lane < 2) fm[nnodes + lane] = integrand<FID>(lane == 0 ? A : B, tab);
                     if constexpr (DIAG) cp1 = clk();
                     bool refine = false;
                     double leafarea = 0.0;
@@ -421,66 +460,63 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         leafarea = larea + rarea;                             // :199
                     }
                     const unsigned long long leafm = __ballot(isnode && valid && !refine) & colmask;
-                    const unsigned dstar = leafm ? (unsigned)__builtin_ctzll(leafm) / nb : (unsigned)D;
+                    const unsigned dstar = leafm ? (unsigned)__builtin_ctzll(leafm) / nb : nlev;
                     if (isnode && valid && d <= dstar && (pp & ((1ull << (D - (int)d)) - 1ull)) == 0ull) {
                         ++acc.tasks;                                          // owner of node (d, kk)
                         acc.maxd = max(acc.maxd, d + 1u);
                         if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
                         if (d == dstar) {
-                            acc.area += leafarea;                             // :199 -> :149
+                            dd_add(acc.hi, acc.lo, leafarea);                 // :199 -> :149
                             ++acc.leaves;
                             if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
                         } else if ((int)d + 1 >= max_depth) {
                             err |= ERRB_DEPTH;
                         }
                     }
-                    // the depth-(D-1) node of a surviving path emits the position's depth-D record
-                    alive = isnode && valid && (int)d == D - 1 && dstar >= (unsigned)D && D < max_depth;
-                    if (alive) {
-                        if (pp & 1ull) { l = mid; fl = fmid; } else { r = mid; fr = fmid; }
-                    }
+                    // a surviving position node emits its children pair (depth D + 1)
+                    alive = isnode && valid && (int)d == D && dstar >= nlev && D + 1 < max_depth;
                     if constexpr (DIAG) cp2 = clk();
                 } else {
-                    for (unsigned q0 = 0; q0 < npairs + 2; q0 += 64) {
+                    for (unsigned q0 = 0; q0 < nnodes + 2; q0 += 64) {
                         const unsigned q = q0 + lane;
-                        if (q < npairs + 2) {
+                        if (q < nnodes + 2) {
                             double x;
-                            if (q < npairs) {
+                            if (q < nnodes) {
                                 const unsigned d = q / nb, kk = q % nb;
                                 bool valid;
                                 const unsigned long long pp = position(kk, valid);
                                 const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
                                 double ll = A, rr = B;
                                 for (unsigned i = 0; i < d; ++i) {
-                                    const double m = (ll + rr) / 2;
-                                    if ((anc >> (d - 1 - i)) & 1ull) ll = m; else rr = m;
+                                    const double mm = (ll + rr) / 2;
+                                    if ((anc >> (d - 1 - i)) & 1ull) ll = mm; else rr = mm;
                                 }
                                 x = (ll + rr) / 2;
                             } else {
-                                x = (q == npairs) ? A : B;
+                                x = (q == nnodes) ? A : B;
                             }
                             fm[q] = integrand<FID>(x, tab);
                         }
                     }
                     if constexpr (DIAG) cp1 = clk();
-                    for (unsigned q0 = 0; q0 < npairs; q0 += 64) {
+                    for (unsigned q0 = 0; q0 < nnodes; q0 += 64) {
                         const unsigned q = q0 + lane;
-                        if (q < npairs) {
+                        if (q < nnodes) {
                             const unsigned d = q / nb, kk = q % nb;
                             bool valid;
                             const unsigned long long pp = position(kk, valid);
                             const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
                             double ll = A, rr = B;
-                            unsigned li = npairs, ri = npairs + 1;
+                            unsigned li = nnodes, ri = nnodes + 1;
                             for (unsigned i = 0; i < d; ++i) {
-                                const double m = (ll + rr) / 2;
-                                if ((anc >> (d - 1 - i)) & 1ull) { ll = m; li = i * nb + kk; } else { rr = m; ri = i * nb + kk; }
+                                const double mm = (ll + rr) / 2;
+                                if ((anc >> (d - 1 - i)) & 1ull) { ll = mm; li = i * nb + kk; } else { rr = mm; ri = i * nb + kk; }
                             }
-                            const double fll = fm[li], frr = fm[ri], fmid = fm[q];
-                            const double mid = (ll + rr) / 2;
+                            const double fll = fm[li], frr = fm[ri], fmd = fm[q];
+                            const double mm = (ll + rr) / 2;
                             const double lrarea = (fll + frr) * (rr - ll) / 2;    // :185
-                            const double larea = (fll + fmid) * (mid - ll) / 2;   // :189
-                            const double rarea = (fmid + frr) * (rr - mid) / 2;   // :190
+                            const double larea = (fll + fmd) * (mm - ll) / 2;     // :189
+                            const double rarea = (fmd + frr) * (rr - mm) / 2;     // :190
                             flag[q] = fabs((larea + rarea) - lrarea) > eps ? 1u : 0u;   // :191
                             leafa[q] = larea + rarea;                             // :199
                         }
@@ -491,34 +527,36 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     bool valid = false;
                     const unsigned long long pp = (kk < nb) ? position(kk, valid) : 0ull;
                     unsigned long long fmask = 0;
-                    for (int d = 0; d < D; ++d)
-                        fmask |= (unsigned long long)(flag[(unsigned)d * nb + (kk < nb ? kk : 0u)] & 1u) << d;
-                    const int dstar = (int)__builtin_ctzll(~fmask);   // first depth that does not refine (D if none)
+                    for (unsigned d = 0; d < nlev; ++d)
+                        fmask |= (unsigned long long)(flag[d * nb + (kk < nb ? kk : 0u)] & 1u) << d;
+                    const unsigned dstar = (unsigned)__builtin_ctzll(~fmask);   // first depth that does not refine
                     if (valid) {
-                        const int dlast = min(dstar, D - 1);
-                        for (int d = 0; d <= dlast; ++d) {
-                            if ((pp & ((1ull << (D - d)) - 1ull)) == 0ull) {   // owner of node (d, kk)
+                        const unsigned dlast = min(dstar, (unsigned)D);
+                        for (unsigned d = 0; d <= dlast; ++d) {
+                            if ((pp & ((1ull << (D - (int)d)) - 1ull)) == 0ull) {   // owner of node (d, kk)
                                 ++acc.tasks;
-                                acc.maxd = max(acc.maxd, (unsigned)d + 1u);
+                                acc.maxd = max(acc.maxd, d + 1u);
                                 if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
                                 if (d == dstar) {
-                                    acc.area += leafa[(unsigned)d * nb + kk];          // :199 -> :149
+                                    dd_add(acc.hi, acc.lo, leafa[d * nb + kk]);   // :199 -> :149
                                     ++acc.leaves;
                                     if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
-                                } else if (d + 1 >= max_depth) {
+                                } else if ((int)d + 1 >= max_depth) {
                                     err |= ERRB_DEPTH;
                                 }
                             }
                         }
-                        alive = dstar >= D && D < max_depth;
+                        alive = dstar >= nlev && D + 1 < max_depth;
                         if (alive) {
-                            unsigned li = npairs, ri = npairs + 1;
+                            unsigned li = nnodes, ri = nnodes + 1;
                             for (int i = 0; i < D; ++i) {
-                                const double m = (l + r) / 2;
-                                if ((pp >> (D - 1 - i)) & 1ull) { l = m; li = (unsigned)i * nb + kk; } else { r = m; ri = (unsigned)i * nb + kk; }
+                                const double mm = (l + r) / 2;
+                                if ((pp >> (D - 1 - i)) & 1ull) { l = mm; li = (unsigned)i * nb + kk; } else { r = mm; ri = (unsigned)i * nb + kk; }
                             }
                             fl = fm[li];
                             fr = fm[ri];
+                            mid = (l + r) / 2;
+                            fmid = fm[(unsigned)D * nb + kk];
                         }
                     }
                 }
@@ -526,7 +564,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned long long am = __ballot(alive);
                 if (alive) {
                     const unsigned j = base + mbcnt(am);
-                    s_l[j] = l; s_r[j] = r; s_fl[j] = fl; s_fr[j] = fr; s_dt[j] = (unsigned)D | ((unsigned)p << 8);
+                    s_a[j] = l; s_m[j] = mid; s_b[j] = r; s_fa[j] = fl; s_fm[j] = fmid; s_fb[j] = fr;   // :192-197
+                    s_dt[j] = (unsigned)(D + 1) | ((unsigned)p << 8);
                 }
                 bot = 0;
                 top = (unsigned)__popcll(am);
@@ -593,8 +632,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned pt = S.ptop;
             for (unsigned i = lane; i < cnt; i += 64) {
                 const unsigned j = POOL0 + ((pt + i) & (PCAP - 1));
-                s_l[j] = ld_wt(&c->l[i]); s_r[j] = ld_wt(&c->r[i]); s_fl[j] = ld_wt(&c->fl[i]);
-                s_fr[j] = ld_wt(&c->fr[i]); s_dt[j] = ld_wt(&c->dt[i]);
+                s_a[j] = ld_wt(&c->a[i]); s_m[j] = ld_wt(&c->m[i]); s_b[j] = ld_wt(&c->b[i]);
+                s_fa[j] = ld_wt(&c->fa[i]); s_fm[j] = ld_wt(&c->fm[i]); s_fb[j] = ld_wt(&c->fb[i]);
+                s_dt[j] = ld_wt(&c->dt[i]);
             }
             if (lane == 0) {
                 S.ptop = pt + cnt;
@@ -615,12 +655,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             continue;
         }
 
-        // ---- keep the ring from overflowing: move its bottom 64 records to the pool, else to HBM
-        if (size > (unsigned)WCAP - 64u * (unsigned)P.ilp) {
+        // ---- keep the ring from overflowing: its bottom 64 pairs go to the cellar, else the pool,
+        //      else an HBM chunk
+        if (size > (unsigned)(WCAP - 64)) {
             if (ctop + 64u <= (unsigned)CCAP) {
-                // the ring's bottom 64 records go down to this wave's cellar (no lock)
                 const unsigned i = ctop + lane, j = base + ring_slot(bot + lane);
-                cel->l[i] = s_l[j]; cel->r[i] = s_r[j]; cel->fl[i] = s_fl[j]; cel->fr[i] = s_fr[j]; cel->dt[i] = s_dt[j];
+                cel->a[i] = s_a[j]; cel->m[i] = s_m[j]; cel->b[i] = s_b[j];
+                cel->fa[i] = s_fa[j]; cel->fm[i] = s_fm[j]; cel->fb[i] = s_fb[j]; cel->dt[i] = s_dt[j];
                 ctop += 64u;
                 bot += 64u;
                 if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], 64ull); }
@@ -630,12 +671,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned pt = S.ptop;
             const bool fits = (pt - S.pbot) + 64u <= (unsigned)PCAP;
             if (fits) {
-                copy_rec(R, base + ring_slot(bot + lane), POOL0 + ((pt + lane) & (PCAP - 1)));
+                copy_pair(R, base + ring_slot(bot + lane), POOL0 + ((pt + lane) & (PCAP - 1)));
                 if (lane == 0) S.ptop = pt + 64u;
             }
             wave_unlock(&S.lock, lane);
             if (!fits) {
-                // pool full: spill 64 records to an HBM chunk (tokens first, then publish)
+                // pool full: spill 64 pairs to an HBM chunk (tokens first, then publish)
                 unsigned slot = 0;
                 if (lane == 0) {
                     slot = g_add(&qctl->q_tail.v, 1u);
@@ -647,7 +688,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     const unsigned b = bot;
                     publish_chunk(P, R, slot, 64u, [&](unsigned i) { return base + ring_slot(b + i); }, lane);
                 } else {
-                    err |= ERRB_OVERFLOW;   // records dropped: result invalid, error reported
+                    err |= ERRB_OVERFLOW;   // pairs dropped: result invalid, error reported
                 }
             }
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_POOL_PUSH], 64ull); }
@@ -655,15 +696,19 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             continue;
         }
 
+        ++poll_ctr;
         // ---- feed idle sibling waves
-        if (size >= (unsigned)GIVE_MIN && S.idle > 0 && S.ptop == S.pbot) {
-            const unsigned k = size / 2u;   // <= WCAP / 2
+        if ((poll_ctr % GIVE_ROUNDS) == 0 && size >= (unsigned)GIVE_MIN &&
+            __hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > 0 &&
+            __hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                __hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            const unsigned k = size / 2u;   // <= WCAP / 2 <= PCAP
             wave_lock(&S.lock, lane, lock_spins);
             const unsigned pt = S.ptop;
             const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
             if (fits) {
                 for (unsigned i = lane; i < k; i += 64)
-                    copy_rec(R, base + ring_slot(bot + i), POOL0 + ((pt + i) & (PCAP - 1)));
+                    copy_pair(R, base + ring_slot(bot + i), POOL0 + ((pt + i) & (PCAP - 1)));
                 if (lane == 0) S.ptop = pt + k;
             }
             wave_unlock(&S.lock, lane);
@@ -674,7 +719,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
         }
         // ---- donate to starving workgroups (another CU waits on the HBM queue)
-        if (((++poll_ctr) % POLL_ROUNDS) == 0) {
+        if ((poll_ctr % POLL_ROUNDS) == 0) {
             unsigned slot = 0xffffffffu;
             if (lane == 0) {
                 if ((int)(seen_head - seen_tail) > 0) {
@@ -721,88 +766,88 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
         }
 
-        // ---- one round: pop up to 64*K records from the top of this wave's ring, K per lane
+        // ---- running low: fetch the next 64 cellar pairs now, land them next iteration
+        if (ctop > 0 && size <= (unsigned)PF_BELOW) {
+            pf_n = min(ctop, 64u);
+            ctop -= pf_n;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's own spills have landed
+            if (lane < pf_n) {
+                const unsigned i = ctop + lane;
+                pf_a = ld_wt(&cel->a[i]); pf_m = ld_wt(&cel->m[i]); pf_b = ld_wt(&cel->b[i]);
+                pf_fa = ld_wt(&cel->fa[i]); pf_fm = ld_wt(&cel->fm[i]); pf_fb = ld_wt(&cel->fb[i]);
+                pf_dt = ld_wt(&cel->dt[i]);
+            }
+            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }
+        }
+
+        // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
+        //      tasks of a pair are evaluated together (two interleaved cosh chains)
         unsigned long long c0 = 0, c1 = 0;
         if constexpr (DIAG) c0 = clk();
-        auto do_round = [&](auto kc) -> unsigned {
-            constexpr int K = decltype(kc)::value;
-            const unsigned n = min(size, 64u * K);
-            const unsigned b0 = top - n;
-            double l[K], r[K], fl[K], fr[K];
-            unsigned dt[K];
-            bool act[K], solo[K], refine[K];
-            bool mixed = false;
+        const unsigned n = min(size, 64u);
+        const unsigned b0 = top - n;
+        const bool act = lane < n;
+        double pa = 1.0, pm = 1.0, pb = 1.0, pfa = 0.0, pfm = 0.0, pfb = 0.0;
+        unsigned dt = 0;
+        if (act) {
+            const unsigned j = base + ring_slot(b0 + lane);
+            pa = s_a[j]; pm = s_m[j]; pb = s_b[j]; pfa = s_fa[j]; pfm = s_fm[j]; pfb = s_fb[j]; dt = s_dt[j];
+        }
+        const unsigned d = dt & 255u;
+        const int rtag = (int)((dt >> 8) & 255u);
+        const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
+        Step st[2];
+        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st);
+        bool refine[2] = {false, false};
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                act[k] = lane + 64u * k < n;
-                l[k] = 1.0; r[k] = 1.0; fl[k] = 0.0; fr[k] = 0.0; dt[k] = 0;
-                if (act[k]) {
-                    const unsigned j = base + ring_slot(b0 + 64u * k + lane);
-                    l[k] = s_l[j]; r[k] = s_r[j]; fl[k] = s_fl[j]; fr[k] = s_fr[j]; dt[k] = s_dt[j];
-                }
-                mixed |= act[k] && (int)(dt[k] >> 8) != tag;
-                solo[k] = false;
-                refine[k] = false;
+        for (int k = 0; k < 2; ++k) {
+            if (act && st[k].refine) {
+                if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
+                else refine[k] = true;
             }
-            // records of another integral than the accumulators': flush, then follow lane 0's
-            // integral; records still of a third one account for themselves (rare: pool/queue moves)
-            if (__ballot(mixed)) {
-                flush_acc(P, acc, tag, lane);
-                tag = __shfl((int)(dt[0] >> 8), 0, 64);
-#pragma unroll
-                for (int k = 0; k < K; ++k) solo[k] = act[k] && (int)(dt[k] >> 8) != tag;
+        }
+        // accounting, one pass per integral present in the round (almost always one: pairs of
+        // several integrals meet only after pool / queue moves); a new integral flushes the old
+        unsigned long long todo = __ballot(act);
+        while (todo) {
+            const int t = __shfl(rtag, (int)__builtin_ctzll(todo), 64);
+            if (t != tag) {
+                flush_acc(P, acc, tag, lane, w_all);
+                tag = t;
                 if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_MIXED_ROUNDS], 1ull); }
             }
-            Step st[K];
-            task_step_k<FID, K>(l, r, fl, fr, eps, tab, st);
+            const bool mine = act && rtag == t;
+            if (mine) {
+                acc.tasks += 2u;
+                acc.maxd = max(acc.maxd, d + 1u);
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (!act[k]) continue;
-                const unsigned d = dt[k] & 255u;
-                const int rtag = (int)(dt[k] >> 8);
-                if (HIST) atomicAdd(&P.ctls[P.first_slot + rtag].hist[d], 1ull);
-                const bool leaf = !st[k].refine;
-                if (st[k].refine) {
-                    if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
-                    else refine[k] = true;
-                } else if (HIST) {
-                    atomicAdd(&P.ctls[P.first_slot + rtag].hist[AQ_MAX_LEVELS + d], 1ull);
-                }
-                if (!solo[k]) {
-                    ++acc.tasks;
-                    acc.maxd = max(acc.maxd, d + 1u);
-                    if (leaf) {
-                        acc.area += st[k].larea + st[k].rarea;  // :199 -> :149
+                for (int k = 0; k < 2; ++k) {
+                    if (HIST) atomicAdd(&P.ctls[P.first_slot + t].hist[d], 1ull);
+                    if (!st[k].refine) {
+                        acc.hi += st[k].larea + st[k].rarea;   // :199 -> :149 (a lane's own few leaves:
+                                                               // rounding far below the total's ulp)
                         ++acc.leaves;
-                    }
-                } else {
-                    WgPart* w = P.parts + (size_t)(P.first_slot + rtag) * gridDim.x + blockIdx.x;
-                    atomicAdd(&w->tasks, 1ull);
-                    atomicMax(&w->levels, d + 1u);
-                    if (leaf) {
-                        atomicAdd(&w->area, st[k].larea + st[k].rarea);
-                        atomicAdd(&w->leaves, 1ull);
+                        if (HIST) atomicAdd(&P.ctls[P.first_slot + t].hist[AQ_MAX_LEVELS + d], 1ull);
                     }
                 }
             }
-            if constexpr (DIAG) c1 = clk();
-            unsigned pushed = 0;   // children pairs so far this round
+            todo &= ~__ballot(mine);
+        }
+        if constexpr (DIAG) c1 = clk();
+        // each refining task pushes its children as one pair (:192-197)
+        const unsigned long long mask0 = __ballot(refine[0]), mask1 = __ballot(refine[1]);
+        const unsigned cnt0 = (unsigned)__popcll(mask0);
+        const unsigned cdt = (d + 1u) | ((unsigned)rtag << 8);
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const unsigned long long mask = __ballot(refine[k]);
-                if (refine[k]) {
-                    const unsigned pos = b0 + 2u * (pushed + mbcnt(mask));
-                    const unsigned j0 = base + ring_slot(pos), j1 = base + ring_slot(pos + 1u);
-                    const unsigned cdt = dt[k] + 1u;   // depth + 1, same integral
-                    s_l[j0] = l[k];      s_r[j0] = st[k].mid; s_fl[j0] = fl[k];      s_fr[j0] = st[k].fmid; s_dt[j0] = cdt;  // :192-194
-                    s_l[j1] = st[k].mid; s_r[j1] = r[k];      s_fl[j1] = st[k].fmid; s_fr[j1] = fr[k];      s_dt[j1] = cdt;  // :195-197
-                }
-                pushed += (unsigned)__popcll(mask);
+        for (int k = 0; k < 2; ++k) {
+            if (refine[k]) {
+                const unsigned pos = b0 + (k == 0 ? mbcnt(mask0) : cnt0 + mbcnt(mask1));
+                const unsigned j = base + ring_slot(pos);
+                s_a[j] = tl[k]; s_m[j] = st[k].mid; s_b[j] = tr[k];
+                s_fa[j] = tfl[k]; s_fm[j] = st[k].fmid; s_fb[j] = tfr[k]; s_dt[j] = cdt;
             }
-            top = b0 + 2u * pushed;
-            return n;
-        };
-        const unsigned n = P.ilp == 2 ? do_round(std::integral_constant<int, 2>{}) : do_round(std::integral_constant<int, 1>{});
+        }
+        top = b0 + cnt0 + (unsigned)__popcll(mask1);
         if constexpr (DIAG) {
             if (lane == 0) {
                 const unsigned long long c2 = clk();
@@ -813,11 +858,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)size);
                 atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
             }
+            const unsigned nt = 2u * n;
+            if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
         }
     }
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
-    flush_acc(P, acc, tag, lane);
+    flush_acc(P, acc, tag, lane, w_all);
     const unsigned werr = wave_or_u(err);
     if (lane == 0) {
         if (werr) {
@@ -828,6 +875,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (DIAG) {
             atomicAdd(&s_dg[DG_LOCK_SPINS], lock_spins);
             atomicAdd(&s_dg[DG_SPILL_RECORDS], spilled);
+            atomicAdd(&s_dg[DG_C_LOOP], clk() - cl0);
         }
     }
     if constexpr (DIAG) {

@@ -179,22 +179,24 @@ __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsig
 // Gather n slots' totals into a caller device buffer as f64 [area, tasks, accepted, error] rows,
 // ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot sums the
 // slot's per-workgroup partials in a fixed order.
-__global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts, int G, int first, int n, int nslots,
-                                                double* __restrict__ out) {
-    __shared__ double s_a[4];
+__global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts, const double2* __restrict__ warea,
+                                                int G, int first, int n, int nslots, double* __restrict__ out) {
+    __shared__ double s_h[4], s_lo[4];
     __shared__ unsigned long long s_t[4], s_l[4];
     __shared__ unsigned s_e[4];
-    const WgPart* w = parts + (size_t)((first + (int)blockIdx.x) % nslots) * G;
-    double a = 0.0;
+    const int slot = (first + (int)blockIdx.x) % nslots;
+    const WgPart* w = parts + (size_t)slot * G;
+    const double2* wa = warea + (size_t)slot * G * NW;
+    double hi = 0.0, lo = 0.0;
     unsigned long long t = 0, l = 0;
     unsigned e = 0;
     for (int i = threadIdx.x; i < G; i += blockDim.x) {
-        a += w[i].area;
         t += w[i].tasks;
         l += w[i].leaves;
         e |= w[i].error;
     }
-    a = wave_sum(a);
+    for (int i = threadIdx.x; i < G * NW; i += blockDim.x) dd_add_dd(hi, lo, wa[i].x, wa[i].y);
+    wave_sum_dd(hi, lo);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         t += __shfl_xor(t, o, 64);
@@ -202,15 +204,15 @@ __global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts
         e |= (unsigned)__shfl_xor((int)e, o, 64);
     }
     const unsigned wv = threadIdx.x >> 6;
-    if (lane_id() == 0) { s_a[wv] = a; s_t[wv] = t; s_l[wv] = l; s_e[wv] = e; }
+    if (lane_id() == 0) { s_h[wv] = hi; s_lo[wv] = lo; s_t[wv] = t; s_l[wv] = l; s_e[wv] = e; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double A = 0.0;
+        double H = 0.0, Lo = 0.0;
         unsigned long long T = 0, L = 0;
         unsigned E = 0;
-        for (int k = 0; k < 4; ++k) { A += s_a[k]; T += s_t[k]; L += s_l[k]; E |= s_e[k]; }
+        for (int k = 0; k < 4; ++k) { dd_add_dd(H, Lo, s_h[k], s_lo[k]); T += s_t[k]; L += s_l[k]; E |= s_e[k]; }
         double* o = out + 4 * blockIdx.x;
-        o[0] = A;
+        o[0] = H + Lo;
         o[1] = (double)T;
         o[2] = (double)L;
         o[3] = (double)E;
@@ -227,7 +229,7 @@ using namespace aq;
 namespace {
 
 constexpr int NSLOTS = 256;
-constexpr unsigned QCAP = 16384;  // HBM queue slots (16384 x 17 KiB = 273 MiB)
+constexpr unsigned QCAP = 16384;  // HBM queue slots (16384 x 13.4 KiB = 219 MiB)
 static_assert(MAXK <= NSLOTS, "a launch's integrals need distinct slots");
 
 #define AQ_HIP(call)                                                                  \
@@ -247,9 +249,9 @@ int err_from_bits(unsigned bits) {
     return AQ_OK;
 }
 
-int ceil_log2(unsigned long long v) {
+int floor_log2(unsigned long long v) {
     int d = 0;
-    while ((1ull << d) < v) ++d;
+    while ((2ull << d) <= v) ++d;
     return d;
 }
 
@@ -284,6 +286,8 @@ struct aq_ctx {
     ExpEntry* d_tab = nullptr;
     Ctl* d_ctl = nullptr;              // NSLOTS control blocks (queue + per-integral histograms)
     WgPart* d_parts = nullptr;         // NSLOTS x grid per-workgroup partials
+    double2* d_warea = nullptr;        // NSLOTS x grid*NW per-wave double-double areas
+    double2* h_warea = nullptr;        // pinned, grid*NW entries
     bool dirty[NSLOTS] = {};           // slot's ctl / parts used since they were last zeroed
     bool slot_hist[NSLOTS] = {};
     double2* d_bounds = nullptr;       // NSLOTS {a, b}
@@ -293,7 +297,6 @@ struct aq_ctx {
     unsigned* d_ready = nullptr;
     unsigned epoch = 0;
     int gsplit_env = 0;                // AQ_GSPLIT: waves per job of a multi-integral launch (0 = default)
-    int ilp_env = 0;                   // AQ_ILP: records per lane per round (0 = default)
     // level path
     DevResults* d_lres = nullptr;
     Rec* d_front[2] = {nullptr, nullptr};
@@ -333,6 +336,8 @@ int ensure_clean(aq_ctx* c, int s, int k) {
     AQ_HIP(hipMemsetAsync(c->d_ctl + s, 0, sizeof(Ctl) * (size_t)(e - s), c->stream));
     AQ_HIP(hipMemsetAsync(c->d_parts + (size_t)s * c->grid, 0, sizeof(WgPart) * (size_t)(e - s) * c->grid,
                           c->stream));
+    AQ_HIP(hipMemsetAsync(c->d_warea + (size_t)s * c->grid * NW, 0, sizeof(double2) * (size_t)(e - s) * c->grid * NW,
+                          c->stream));
     return AQ_OK;
 }
 
@@ -359,14 +364,14 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     if (ctx->gsplit_env > 0) gs = ctx->gsplit_env;
     while (gs > 1 && (G * NW) % gs != 0) gs >>= 1;
     P.shares = G * NW / gs;
-    P.ilp = ctx->ilp_env == 1 || ctx->ilp_env == 2 ? ctx->ilp_env : DEFAULT_ILP;
-    P.D = ceil_log2((unsigned long long)P.shares * (unsigned long long)nshards) + S_W;
+    P.D = floor_log2((unsigned long long)P.shares * (unsigned long long)nshards) + S_W;
     P.epoch = ++ctx->epoch;
     if (P.epoch == 0) P.epoch = ++ctx->epoch;
     P.qcap = QCAP;
     P.timeout_ticks = 100000000ull * 20ull;  // 20 s of the 100 MHz realtime clock
     P.ctls = ctx->d_ctl;
     P.parts = ctx->d_parts;
+    P.warea = ctx->d_warea;
     P.diag = ctx->d_diag;
     P.chunks = ctx->d_chunks;
     P.cellar = ctx->d_cellar;
@@ -414,15 +419,20 @@ void fill_result(const HostOut& h, aq_result* out) {
 int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
     AQ_HIP(hipMemcpyAsync(ctx->h_parts, ctx->d_parts + (size_t)slot * ctx->grid, sizeof(WgPart) * (size_t)ctx->grid,
                           hipMemcpyDeviceToHost, ctx->stream));
+    const size_t nw = (size_t)ctx->grid * NW;
+    AQ_HIP(hipMemcpyAsync(ctx->h_warea, ctx->d_warea + (size_t)slot * nw, sizeof(double2) * nw, hipMemcpyDeviceToHost,
+                          ctx->stream));
     if (ctx->slot_hist[slot])
         AQ_HIP(hipMemcpyAsync(ctx->h_hist, ctx->d_ctl[slot].hist, sizeof(unsigned long long) * 2 * AQ_MAX_LEVELS,
                               hipMemcpyDeviceToHost, ctx->stream));
     AQ_HIP(hipStreamSynchronize(ctx->stream));
     HostOut& h = ctx->last;
     h = HostOut();
+    double hi = 0.0, lo = 0.0;
+    for (size_t i = 0; i < nw; ++i) dd_add_dd(hi, lo, ctx->h_warea[i].x, ctx->h_warea[i].y);
+    h.area = hi + lo;
     for (int i = 0; i < ctx->grid; ++i) {
         const WgPart& w = ctx->h_parts[i];
-        h.area += w.area;
         h.tasks += w.tasks;
         h.leaves += w.leaves;
         h.spilled += w.spilled;
@@ -494,7 +504,6 @@ int aq_ctx_create(int device, aq_ctx** out) {
     // resident, because idle workgroups wait on the queue for busy ones.
     c->grid = std::min(c->num_cus, MAXG);
     if (const char* e = getenv("AQ_GSPLIT")) c->gsplit_env = atoi(e);
-    if (const char* e = getenv("AQ_ILP")) c->ilp_env = atoi(e);
     AQ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     AQ_HIP(hipMalloc(&c->d_tab, sizeof(ExpEntry) * 128));
     AQ_HIP(hipMemcpy(c->d_tab, aq_exp_tab_host, sizeof(ExpEntry) * 128, hipMemcpyHostToDevice));
@@ -502,6 +511,9 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipMemset(c->d_ctl, 0, sizeof(Ctl) * NSLOTS));
     AQ_HIP(hipMalloc(&c->d_parts, sizeof(WgPart) * (size_t)NSLOTS * c->grid));
     AQ_HIP(hipMemset(c->d_parts, 0, sizeof(WgPart) * (size_t)NSLOTS * c->grid));
+    AQ_HIP(hipMalloc(&c->d_warea, sizeof(double2) * (size_t)NSLOTS * c->grid * NW));
+    AQ_HIP(hipMemset(c->d_warea, 0, sizeof(double2) * (size_t)NSLOTS * c->grid * NW));
+    AQ_HIP(hipHostMalloc(&c->h_warea, sizeof(double2) * (size_t)c->grid * NW, hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_bounds, sizeof(double2) * NSLOTS));
     AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS, hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_chunks, sizeof(Chunk) * (size_t)QCAP));
@@ -527,6 +539,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_tab);
     (void)hipFree(c->d_ctl);
     (void)hipFree(c->d_parts);
+    (void)hipFree(c->d_warea);
     (void)hipFree(c->d_bounds);
     (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_cellar);
@@ -540,6 +553,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_y);
     if (c->h_bounds) (void)hipHostFree(c->h_bounds);
     if (c->h_parts) (void)hipHostFree(c->h_parts);
+    if (c->h_warea) (void)hipHostFree(c->h_warea);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->h_lres) (void)hipHostFree(c->h_lres);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -547,6 +561,7 @@ void aq_ctx_destroy(aq_ctx* c) {
 }
 
 int aq_ctx_num_cus(const aq_ctx* c) { return c ? c->num_cus : 0; }
+int aq_ctx_num_workers(const aq_ctx* c) { return c ? c->grid * NW : 0; }
 
 int aq_set_level_histograms(aq_ctx* c, int enable) {
     if (!c) return AQ_EINVAL;
@@ -605,8 +620,8 @@ int aq_gather_results(aq_ctx* ctx, int first_slot, int n, void* d_out) {
     if (!ctx || !d_out || n < 0 || n > NSLOTS || first_slot < 0 || first_slot >= NSLOTS) return AQ_EINVAL;
     if (n == 0) return AQ_OK;
     AQ_HIP(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_parts, ctx->grid, first_slot, n, NSLOTS,
-                       (double*)d_out);
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_parts, ctx->d_warea, ctx->grid, first_slot,
+                       n, NSLOTS, (double*)d_out);
     AQ_HIP(hipGetLastError());
     return AQ_OK;
 }

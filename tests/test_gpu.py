@@ -2,6 +2,7 @@
 reference's golden vectors. Bar: interval counts (tasks, accepted, per-level histograms) bit-exact;
 area within 1e-12 relative of the quad-precision Σ of leaf areas (BASELINE.json north_star);
 device cosh bit-identical to host glibc 2.35."""
+import math
 import os
 import subprocess
 
@@ -84,6 +85,11 @@ def test_persistent_tree_parity(ctx, trees, name):
     assert r.tasks_per_level == g["tasks_per_level"]
     assert r.leaves_per_level == g["leaves_per_level"]
     assert _area_ok(r.area, g["area_quad"]), (r.area, g["area_quad"])
+    if g["integrand"] == "cosh4":   # F bit-exact (sin(1/x) is faithful only): leaf areas are the
+        # reference's; lanes sum their own few leaves in double, everything above is double-double,
+        # so the area is within 1 ulp of the correctly rounded sum of the leaf areas
+        want = float(g["area_quad"])
+        assert abs(r.area - want) <= math.ulp(want), (r.area.hex(), want.hex())
     assert sum(r.tasks_per_cu.values()) == r.tasks
     assert r.n_cu == len(r.tasks_per_cu) >= 1
 
@@ -119,7 +125,7 @@ def test_shards_match_oracle_partition(ctx, trees, oracle, name, nshards):
     area = 0.0
     for s in range(nshards):
         r = ctx.integrate_shard(p, s, nshards)
-        o = oracle.integrate_shard(s, nshards, G=ctx.num_cus * 8, S=2, integrand=p.integrand, a=p.a, b=p.b,
+        o = oracle.integrate_shard(s, nshards, G=ctx.num_workers, S=2, integrand=p.integrand, a=p.a, b=p.b,
                                    eps=p.eps)
         assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
         assert r.tasks_per_level == o.tasks_per_level
@@ -213,7 +219,7 @@ def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
 
 
 def test_many_sharded(ctx, oracle, trees):
-    """Sharded multi-integral launches: per-shard counts match the oracle partition (G*8 wave workers)."""
+    """Sharded multi-integral launches: per-shard counts match the oracle partition (one share per wave worker)."""
     g = trees["cosh4_eps1e-10"]
     tot_t = tot_l = 0
     for s in range(2):
@@ -243,6 +249,7 @@ def test_large_jobs_and_cellar(trees, monkeypatch):
             assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"])
             assert _area_ok(r.area, g["area_quad"])
         col = dict(zip(f, d.T))
-        assert col["cellar_out"].sum() > 0 and col["cellar_out"].sum() == col["cellar_in"].sum()
+        assert col["cellar_out"].sum() > 0
+        assert col["cellar_out"].sum() == col["cellar_in"].sum() + col["prefetch"].sum()
     finally:
         c.close()

@@ -34,9 +34,17 @@ def summarize(d, f):
     s["cyc_idle_per_wg_p50"] = float(np.median(col["c_idle"]))
     s["cyc_round_per_wg_p50"] = float(np.median(col["c_round"]))
     s["cyc_seed_per_wg_p50"] = float(np.median(col["c_seed"]))
+    s["cyc_refill_per_wg_p50"] = float(np.median(col["c_refill"]))
+    s["cyc_loop_per_wg_p50"] = float(np.median(col["c_loop"]))   # sum over the workgroup's waves
+    s["tasks_per_round"] = float(col["active_tasks"].sum() / max(col["rounds"].sum(), 1))
+    # shares of the waves' loop time
+    loop = max(float(np.median(col["c_loop"])), 1.0)
+    s["share_of_loop"] = {k: round(float(np.median(col[c])) / loop, 3)
+                          for k, c in (("round", "c_round"), ("seed", "c_seed"), ("idle_pool", "c_idle"),
+                                       ("refill", "c_refill"))}
     s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
                   "sum": col["tasks"].sum()}
-    for k in ("leads", "pool_push", "pool_take", "give", "cellar_in", "cellar_out", "lock_spins", "spill_records", "chunks_out", "chunks_in",
+    for k in ("leads", "pool_push", "pool_take", "give", "cellar_in", "cellar_out", "prefetch", "lock_spins", "spill_records", "chunks_out", "chunks_in",
               "records_out", "records_in", "seed_calls", "mixed_rounds"):
         s[k] = {"sum": col[k].sum(), "max": col[k].max()}
     s["t_wait_us_p50"] = float(np.median(col["t_wait"])) / 100.0
