@@ -85,7 +85,7 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=2048)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -145,7 +145,6 @@ def main():
     ctx.synchronize()
 
     K = args.steps
-    buf = torch.zeros((kmax, 4), dtype=torch.float64, device="cuda")
     totals = torch.zeros((K, 4), dtype=torch.float64, device="cuda")
     ctx.kernel_timing(True)
     barrier()
@@ -153,15 +152,15 @@ def main():
     t0 = time.perf_counter()
     done = 0
     while done < K:
+        # launches queue back to back on the context's stream: each gathers its slots' results into
+        # its rows of `totals` (device memory), and the next launch re-zeroes the slots after that
         m = min(K - done, kmax)
         launch(m)
-        ctx.gather_results(0, m, buf.data_ptr())
-        ctx.synchronize()
-        chunk = buf[:m]
-        if world > 1:
-            dist.all_reduce(chunk, op=dist.ReduceOp.SUM)
-        totals[done:done + m] = chunk
+        ctx.gather_results(0, m, totals.data_ptr() + done * 4 * totals.element_size())
         done += m
+    ctx.synchronize()
+    if world > 1:
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM)   # shard partials -> whole integrals
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()

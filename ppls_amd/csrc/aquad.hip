@@ -229,6 +229,7 @@ using namespace aq;
 namespace {
 
 constexpr int NSLOTS = 256;
+constexpr int NSTAGE = 4;          // pinned bounds staging buffers
 constexpr unsigned QCAP = 16384;  // HBM queue slots (16384 x 13.4 KiB = 219 MiB)
 static_assert(MAXK <= NSLOTS, "a launch's integrals need distinct slots");
 
@@ -291,7 +292,10 @@ struct aq_ctx {
     bool dirty[NSLOTS] = {};           // slot's ctl / parts used since they were last zeroed
     bool slot_hist[NSLOTS] = {};
     double2* d_bounds = nullptr;       // NSLOTS {a, b}
-    double2* h_bounds = nullptr;       // pinned staging, NSLOTS
+    double2* h_bounds = nullptr;       // pinned staging ring, NSTAGE x NSLOTS (a launch's copy may still be
+                                       // pending when the host queues the next launch)
+    hipEvent_t stage_ev[NSTAGE] = {};  // recorded after each staging copy
+    int stage = 0;
     Chunk* d_chunks = nullptr;
     Cellar* d_cellar = nullptr;        // grid * NW per-wave HBM overflow stacks
     unsigned* d_ready = nullptr;
@@ -347,9 +351,14 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     const int G = ctx->grid;
     int rc = ensure_clean(ctx, first_slot, k);
     if (rc) return rc;
-    for (int i = 0; i < k; ++i) ctx->h_bounds[first_slot + i] = make_double2(a[i], b[i]);
-    AQ_HIP(hipMemcpyAsync(ctx->d_bounds + first_slot, ctx->h_bounds + first_slot, sizeof(double2) * (size_t)k,
+    const int st = ctx->stage;
+    ctx->stage = (st + 1) % NSTAGE;
+    AQ_HIP(hipEventSynchronize(ctx->stage_ev[st]));   // the copy that last used this buffer is done
+    double2* hb = ctx->h_bounds + (size_t)st * NSLOTS;
+    for (int i = 0; i < k; ++i) hb[i] = make_double2(a[i], b[i]);
+    AQ_HIP(hipMemcpyAsync(ctx->d_bounds + first_slot, hb, sizeof(double2) * (size_t)k,
                           hipMemcpyHostToDevice, ctx->stream));
+    AQ_HIP(hipEventRecord(ctx->stage_ev[st], ctx->stream));
     StreamParams P{};
     P.bounds = ctx->d_bounds + first_slot;
     P.nprob = k;
@@ -515,7 +524,11 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipMemset(c->d_warea, 0, sizeof(double2) * (size_t)NSLOTS * c->grid * NW));
     AQ_HIP(hipHostMalloc(&c->h_warea, sizeof(double2) * (size_t)c->grid * NW, hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_bounds, sizeof(double2) * NSLOTS));
-    AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS, hipHostMallocDefault));
+    AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS * NSTAGE, hipHostMallocDefault));
+    for (int i = 0; i < NSTAGE; ++i) {
+        AQ_HIP(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+        AQ_HIP(hipEventRecord(c->stage_ev[i], c->stream));
+    }
     AQ_HIP(hipMalloc(&c->d_chunks, sizeof(Chunk) * (size_t)QCAP));
     AQ_HIP(hipMalloc(&c->d_cellar, sizeof(Cellar) * (size_t)c->grid * NW));
     AQ_HIP(hipMalloc(&c->d_ready, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
@@ -552,6 +565,8 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_x);
     (void)hipFree(c->d_y);
     if (c->h_bounds) (void)hipHostFree(c->h_bounds);
+    for (int i = 0; i < NSTAGE; ++i)
+        if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
     if (c->h_parts) (void)hipHostFree(c->h_parts);
     if (c->h_warea) (void)hipHostFree(c->h_warea);
     if (c->h_hist) (void)hipHostFree(c->h_hist);

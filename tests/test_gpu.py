@@ -253,3 +253,28 @@ def test_large_jobs_and_cellar(trees, monkeypatch):
         assert col["cellar_out"].sum() == col["cellar_in"].sum() + col["prefetch"].sum()
     finally:
         c.close()
+
+
+def test_back_to_back_launches_same_slots(ctx, oracle, batch_golden, trees):
+    """Launches queued without a host sync reuse the same slots; each gathers its own results
+    (bounds staging must not be overwritten while a previous copy is pending)."""
+    import torch
+    a1, b1 = oracle.batch_bounds(8)
+    out = torch.zeros((3, 8, 4), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    ctx.set_level_histograms(False)
+    try:
+        for rep in range(3):
+            if rep == 1:
+                ctx.integrate_many_async(np.zeros(8), np.full(8, 5.0), 1e-3, first_slot=0)
+            else:
+                ctx.integrate_many_async(a1, b1, 1e-3, first_slot=0)
+            ctx.gather_results(0, 8, out[rep].data_ptr())
+        ctx.synchronize()
+    finally:
+        ctx.set_level_histograms(True)
+    o = out.cpu().numpy()
+    want = batch_golden["leaves_eps1e-3_first256"][:8]
+    assert [int(v) for v in o[0, :, 2]] == want and [int(v) for v in o[2, :, 2]] == want
+    assert (o[1, :, 2] == trees["cosh4_eps1e-3"]["leaves"]).all()
+    assert (o[:, :, 3] == 0).all()
