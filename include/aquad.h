@@ -74,6 +74,15 @@ int aq_ctx_num_workers(const aq_ctx *ctx);
 /* Per-level task/accepted histograms on the persistent path (default on; a diagnostic the
  * reference does not produce -- pipelined callers switch it off). */
 int aq_set_level_histograms(aq_ctx *ctx, int enable);
+/* Which persistent kernel runs a launch (no reference counterpart: the reference has one schedule,
+ * the MPI bag). AUTO: the lane-DFS kernel for launches of >= 16 integrals, the streaming pair kernel
+ * (HBM work queue between CUs) below that. Counts and areas are identical under every engine; the
+ * engine only changes the schedule (and aq_ctx_num_workers, the share count of a lone integral).
+ * The AQ_ENGINE environment variable ("stream" / "dfs") sets the default of new contexts. */
+#define AQ_ENGINE_AUTO 0
+#define AQ_ENGINE_STREAM 1
+#define AQ_ENGINE_DFS 2
+int aq_set_engine(aq_ctx *ctx, int engine);
 
 /* ---- the hot path ----------------------------------------------------------------------------
  * aq_integrate: farmer(numprocs) + every worker() of one run (:125-208) as ONE persistent HIP

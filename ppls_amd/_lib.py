@@ -7,12 +7,12 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libaquad.so")
+LIB_PATH = os.environ.get("AQ_LIB") or os.path.join(HERE, "_build", "libaquad.so")
 
 # Every symbol include/aquad.h declares (tests check the library exports all of them).
 EXPORTS = (
     "aq_device_count", "aq_ctx_create", "aq_ctx_destroy", "aq_strerror", "aq_ctx_num_cus", "aq_ctx_num_workers",
-    "aq_set_level_histograms",
+    "aq_set_level_histograms", "aq_set_engine",
     "aq_integrate", "aq_integrate_shard", "aq_async_slots", "aq_integrate_async", "aq_fetch",
     "aq_max_integrals_per_launch", "aq_integrate_many_async",
     "aq_synchronize", "aq_gather_results", "aq_integrate_levels", "aq_level_histogram", "aq_tasks_per_cu",
@@ -60,6 +60,7 @@ def load(build_if_missing=True):
         "aq_ctx_num_cus": ([vp], ctypes.c_int),
         "aq_ctx_num_workers": ([vp], ctypes.c_int),
         "aq_set_level_histograms": ([vp, ctypes.c_int], ctypes.c_int),
+        "aq_set_engine": ([vp, ctypes.c_int], ctypes.c_int),
         "aq_integrate": ([vp, P, R], ctypes.c_int),
         "aq_integrate_shard": ([vp, P, ctypes.c_int, ctypes.c_int, R], ctypes.c_int),
         "aq_async_slots": ([], ctypes.c_int),

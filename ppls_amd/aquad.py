@@ -88,7 +88,17 @@ class Context:
         _check(self.L.aq_ctx_create(int(device), ctypes.byref(self._h)), "aq_ctx_create")
         self.device = device
         self.num_cus = self.L.aq_ctx_num_cus(self._h)
-        self.num_workers = self.L.aq_ctx_num_workers(self._h)
+
+    ENGINES = {"auto": 0, "stream": 1, "dfs": 2}
+
+    @property
+    def num_workers(self) -> int:
+        """Shares a lone integral is split into under the current engine (the oracle partition's G)."""
+        return self.L.aq_ctx_num_workers(self._h)
+
+    def set_engine(self, engine: str):
+        """Persistent kernel for later launches: "auto", "stream" (pair rings + HBM queue) or "dfs" (lane DFS)."""
+        _check(self.L.aq_set_engine(self._h, self.ENGINES[engine]), "aq_set_engine")
 
     def close(self):
         if self._h:

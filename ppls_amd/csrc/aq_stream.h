@@ -118,6 +118,8 @@ struct StreamParams {
     Cellar* cellar;                 // [gridDim.x * NW]
     unsigned* ready;
     const ExpEntry* gtab;
+    double2* stk;                   // k_dfs: per-lane DFS stacks [wave][SDEPTH][64] {x, F(x)}
+    unsigned wstride;               // warea entries per slot (>= waves of any engine's grid)
 };
 
 // Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
@@ -212,7 +214,7 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
         atomicAdd(&w->tasks, (unsigned long long)t);
         atomicAdd(&w->leaves, (unsigned long long)l);
         atomicMax(&w->levels, m);
-        double* q = &P.warea[(size_t)(P.first_slot + tag) * gridDim.x * NW + w_all].x;
+        double* q = &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all].x;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
         double h0 = ld_wt(q), l0 = ld_wt(q + 1);
         dd_add_dd(h0, l0, hi, lo);
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
     const unsigned tid = threadIdx.x;
     const unsigned lane = lane_id();
-    const unsigned wid = tid >> 6;
+    const unsigned wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps the wave state in SGPRs
     Ctl* __restrict__ qctl = P.ctls + P.first_slot;
     const LdsPairs R{s_a, s_m, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned long long t_entry = rtc();

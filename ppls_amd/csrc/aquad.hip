@@ -35,6 +35,7 @@
 #include "aq_libm.h"
 #include "aq_device.h"
 #include "aq_stream.h"
+#include "aq_dfs.h"
 
 #pragma clang fp contract(off)
 
@@ -180,13 +181,14 @@ __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsig
 // ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot sums the
 // slot's per-workgroup partials in a fixed order.
 __global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts, const double2* __restrict__ warea,
-                                                int G, int first, int n, int nslots, double* __restrict__ out) {
+                                                int G, int wstride, int first, int n, int nslots,
+                                                double* __restrict__ out) {
     __shared__ double s_h[4], s_lo[4];
     __shared__ unsigned long long s_t[4], s_l[4];
     __shared__ unsigned s_e[4];
     const int slot = (first + (int)blockIdx.x) % nslots;
     const WgPart* w = parts + (size_t)slot * G;
-    const double2* wa = warea + (size_t)slot * G * NW;
+    const double2* wa = warea + (size_t)slot * wstride;
     double hi = 0.0, lo = 0.0;
     unsigned long long t = 0, l = 0;
     unsigned e = 0;
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts
         l += w[i].leaves;
         e |= w[i].error;
     }
-    for (int i = threadIdx.x; i < G * NW; i += blockDim.x) dd_add_dd(hi, lo, wa[i].x, wa[i].y);
+    for (int i = threadIdx.x; i < wstride; i += blockDim.x) dd_add_dd(hi, lo, wa[i].x, wa[i].y);
     wave_sum_dd(hi, lo);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -230,7 +232,8 @@ namespace {
 
 constexpr int NSLOTS = 256;
 constexpr int NSTAGE = 4;          // pinned bounds staging buffers
-constexpr unsigned QCAP = 16384;  // HBM queue slots (16384 x 13.4 KiB = 219 MiB)
+constexpr unsigned QCAP = 16384;
+constexpr int DFS_MIN_K = 16;     // auto engine: launches of at least this many integrals run k_dfs  // HBM queue slots (16384 x 13.4 KiB = 219 MiB)
 static_assert(MAXK <= NSLOTS, "a launch's integrals need distinct slots");
 
 #define AQ_HIP(call)                                                                  \
@@ -300,6 +303,9 @@ struct aq_ctx {
     Cellar* d_cellar = nullptr;        // grid * NW per-wave HBM overflow stacks
     unsigned* d_ready = nullptr;
     unsigned epoch = 0;
+    int engine = AQ_ENGINE_AUTO;       // aq_set_engine
+    int wstride = 0;                   // warea entries per slot: max waves of either engine's grid
+    double2* d_stk = nullptr;          // k_dfs lane stacks, grid * DW * SDEPTH * 64 entries
     int gsplit_env = 0;                // AQ_GSPLIT: waves per job of a multi-integral launch (0 = default)
     // level path
     DevResults* d_lres = nullptr;
@@ -340,15 +346,27 @@ int ensure_clean(aq_ctx* c, int s, int k) {
     AQ_HIP(hipMemsetAsync(c->d_ctl + s, 0, sizeof(Ctl) * (size_t)(e - s), c->stream));
     AQ_HIP(hipMemsetAsync(c->d_parts + (size_t)s * c->grid, 0, sizeof(WgPart) * (size_t)(e - s) * c->grid,
                           c->stream));
-    AQ_HIP(hipMemsetAsync(c->d_warea + (size_t)s * c->grid * NW, 0, sizeof(double2) * (size_t)(e - s) * c->grid * NW,
+    AQ_HIP(hipMemsetAsync(c->d_warea + (size_t)s * c->wstride, 0, sizeof(double2) * (size_t)(e - s) * c->wstride,
                           c->stream));
     return AQ_OK;
 }
+
+// The engine a launch of k integrals runs on: the lane-DFS kernel for multi-integral launches (many
+// jobs, the throughput path), the streaming pair kernel (HBM work queue) for a lone integral.
+bool use_dfs(const aq_ctx* ctx, int k) {
+    if (ctx->engine == AQ_ENGINE_DFS) return true;
+    if (ctx->engine == AQ_ENGINE_STREAM) return false;
+    return k >= DFS_MIN_K;
+}
+
+int engine_waves(const aq_ctx* ctx, bool dfs) { return ctx->grid * (dfs ? DW : NW); }
 
 template <int FID, bool HIST>
 int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double eps, int max_depth, int shard,
                   int nshards, int first_slot) {
     const int G = ctx->grid;
+    const bool dfs = use_dfs(ctx, k);
+    const int W = engine_waves(ctx, dfs);
     int rc = ensure_clean(ctx, first_slot, k);
     if (rc) return rc;
     const int st = ctx->stage;
@@ -371,8 +389,8 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     // multi-integral launch uses gsplit-times larger shares, so one seeding pass feeds more rounds
     int gs = k >= 16 ? DEFAULT_GSPLIT : 1;
     if (ctx->gsplit_env > 0) gs = ctx->gsplit_env;
-    while (gs > 1 && (G * NW) % gs != 0) gs >>= 1;
-    P.shares = G * NW / gs;
+    while (gs > 1 && W % gs != 0) gs >>= 1;
+    P.shares = W / gs;
     P.D = floor_log2((unsigned long long)P.shares * (unsigned long long)nshards) + S_W;
     P.epoch = ++ctx->epoch;
     if (P.epoch == 0) P.epoch = ++ctx->epoch;
@@ -386,6 +404,8 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.cellar = ctx->d_cellar;
     P.ready = ctx->d_ready;
     P.gtab = ctx->d_tab;
+    P.stk = ctx->d_stk;
+    P.wstride = (unsigned)ctx->wstride;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (ctx->timing) {
         if (!ctx->ev_free.empty()) {
@@ -397,10 +417,16 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
         }
         AQ_HIP(hipEventRecord(ev.first, ctx->stream));
     }
-    if (P.diag)
+    if (dfs) {
+        if (P.diag)
+            hipLaunchKernelGGL((k_dfs<FID, HIST, true>), dim3(G), dim3(DPT), 0, ctx->stream, P);
+        else
+            hipLaunchKernelGGL((k_dfs<FID, HIST, false>), dim3(G), dim3(DPT), 0, ctx->stream, P);
+    } else if (P.diag) {
         hipLaunchKernelGGL((k_stream<FID, HIST, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
-    else
+    } else {
         hipLaunchKernelGGL((k_stream<FID, HIST, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
+    }
     AQ_HIP(hipGetLastError());
     if (ctx->timing) {
         AQ_HIP(hipEventRecord(ev.second, ctx->stream));
@@ -428,7 +454,7 @@ void fill_result(const HostOut& h, aq_result* out) {
 int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
     AQ_HIP(hipMemcpyAsync(ctx->h_parts, ctx->d_parts + (size_t)slot * ctx->grid, sizeof(WgPart) * (size_t)ctx->grid,
                           hipMemcpyDeviceToHost, ctx->stream));
-    const size_t nw = (size_t)ctx->grid * NW;
+    const size_t nw = (size_t)ctx->wstride;
     AQ_HIP(hipMemcpyAsync(ctx->h_warea, ctx->d_warea + (size_t)slot * nw, sizeof(double2) * nw, hipMemcpyDeviceToHost,
                           ctx->stream));
     if (ctx->slot_hist[slot])
@@ -512,6 +538,11 @@ int aq_ctx_create(int device, aq_ctx** out) {
     // One workgroup per CU (the LDS rings take most of a CU's LDS); the whole grid must be
     // resident, because idle workgroups wait on the queue for busy ones.
     c->grid = std::min(c->num_cus, MAXG);
+    c->wstride = c->grid * std::max(NW, DW);
+    if (const char* e = getenv("AQ_ENGINE")) {
+        if (!strcmp(e, "stream")) c->engine = AQ_ENGINE_STREAM;
+        else if (!strcmp(e, "dfs")) c->engine = AQ_ENGINE_DFS;
+    }
     if (const char* e = getenv("AQ_GSPLIT")) c->gsplit_env = atoi(e);
     AQ_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     AQ_HIP(hipMalloc(&c->d_tab, sizeof(ExpEntry) * 128));
@@ -520,9 +551,10 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipMemset(c->d_ctl, 0, sizeof(Ctl) * NSLOTS));
     AQ_HIP(hipMalloc(&c->d_parts, sizeof(WgPart) * (size_t)NSLOTS * c->grid));
     AQ_HIP(hipMemset(c->d_parts, 0, sizeof(WgPart) * (size_t)NSLOTS * c->grid));
-    AQ_HIP(hipMalloc(&c->d_warea, sizeof(double2) * (size_t)NSLOTS * c->grid * NW));
-    AQ_HIP(hipMemset(c->d_warea, 0, sizeof(double2) * (size_t)NSLOTS * c->grid * NW));
-    AQ_HIP(hipHostMalloc(&c->h_warea, sizeof(double2) * (size_t)c->grid * NW, hipHostMallocDefault));
+    AQ_HIP(hipMalloc(&c->d_warea, sizeof(double2) * (size_t)NSLOTS * c->wstride));
+    AQ_HIP(hipMemset(c->d_warea, 0, sizeof(double2) * (size_t)NSLOTS * c->wstride));
+    AQ_HIP(hipHostMalloc(&c->h_warea, sizeof(double2) * (size_t)c->wstride, hipHostMallocDefault));
+    AQ_HIP(hipMalloc(&c->d_stk, sizeof(double2) * (size_t)c->grid * DW * SDEPTH * 64));
     AQ_HIP(hipMalloc(&c->d_bounds, sizeof(double2) * NSLOTS));
     AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS * NSTAGE, hipHostMallocDefault));
     for (int i = 0; i < NSTAGE; ++i) {
@@ -556,6 +588,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_bounds);
     (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_cellar);
+    (void)hipFree(c->d_stk);
     (void)hipFree(c->d_ready);
     (void)hipFree(c->d_lres);
     (void)hipFree(c->d_diag);
@@ -576,7 +609,13 @@ void aq_ctx_destroy(aq_ctx* c) {
 }
 
 int aq_ctx_num_cus(const aq_ctx* c) { return c ? c->num_cus : 0; }
-int aq_ctx_num_workers(const aq_ctx* c) { return c ? c->grid * NW : 0; }
+int aq_ctx_num_workers(const aq_ctx* c) { return c ? engine_waves(c, use_dfs(c, 1)) : 0; }
+
+int aq_set_engine(aq_ctx* c, int engine) {
+    if (!c || engine < AQ_ENGINE_AUTO || engine > AQ_ENGINE_DFS) return AQ_EINVAL;
+    c->engine = engine;
+    return AQ_OK;
+}
 
 int aq_set_level_histograms(aq_ctx* c, int enable) {
     if (!c) return AQ_EINVAL;
@@ -635,8 +674,8 @@ int aq_gather_results(aq_ctx* ctx, int first_slot, int n, void* d_out) {
     if (!ctx || !d_out || n < 0 || n > NSLOTS || first_slot < 0 || first_slot >= NSLOTS) return AQ_EINVAL;
     if (n == 0) return AQ_OK;
     AQ_HIP(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_parts, ctx->d_warea, ctx->grid, first_slot,
-                       n, NSLOTS, (double*)d_out);
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_parts, ctx->d_warea, ctx->grid,
+                       ctx->wstride, first_slot, n, NSLOTS, (double*)d_out);
     AQ_HIP(hipGetLastError());
     return AQ_OK;
 }
