@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true",
                     help="skip the one-integral-per-launch latency probe (profiling runs: every dispatch is K-wide)")
-    ap.add_argument("--per-launch", type=int, default=256,
+    ap.add_argument("--per-launch", type=int, default=2048,
                     help="integrals per persistent launch (1 = one launch per integral)")
     args = ap.parse_args()
 

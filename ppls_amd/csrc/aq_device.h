@@ -115,6 +115,17 @@ __device__ __forceinline__ void wave_sum_dd(double& hi, double& lo) {
     }
 }
 
+// Wave-uniform values (readfirstlane). The persistent kernels' loops mix divergent regions with
+// wave-level state; LLVM's uniformity analysis loses track of that state across the joins and would
+// keep it in VGPRs, copied at every join. Re-asserting it once per iteration keeps it in SGPRs.
+__device__ __forceinline__ unsigned uni(unsigned v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned long long uni(unsigned long long v) {
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
+           (unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)v);
+}
+__device__ __forceinline__ bool uni(bool v) { return __builtin_amdgcn_readfirstlane((unsigned)v) != 0u; }
+
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
 
 __device__ __forceinline__ unsigned long long clk() {

@@ -47,12 +47,6 @@ struct DfsLds {
     unsigned sflag[DW][DSCR];           // seeding: node refines (slow path)
 };
 
-__device__ __forceinline__ unsigned uni(unsigned v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ unsigned long long uni(unsigned long long v) {
-    return ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)) << 32) |
-           (unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)v);
-}
 
 // Flush one accumulation slot of a wave: per-lane areas reduce in double-double into the wave's own
 // partial (plain read-modify-write: no other wave touches it), counts go to this workgroup's
@@ -81,7 +75,6 @@ template <int FID, bool HIST, bool DIAG>
 __global__ __launch_bounds__(DPT) void k_dfs(StreamParams P) {
     __shared__ DfsLds L;
     __shared__ ExpEntry tab[128];
-    __shared__ double2 s_bounds[MAXK];
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
 
     const unsigned tid = threadIdx.x;
@@ -92,10 +85,8 @@ __global__ __launch_bounds__(DPT) void k_dfs(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += DPT) s_dg[i] = 0ull;
     }
-    if (tid < (unsigned)P.nprob && tid < (unsigned)MAXK) {
-        P.parts[(size_t)(P.first_slot + tid) * gridDim.x + blockIdx.x].cu = cu_slot();
-        s_bounds[tid] = P.bounds[tid];
-    }
+    for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
+        P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
@@ -226,7 +217,7 @@ __global__ __launch_bounds__(DPT) void k_dfs(StreamParams P) {
                 const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
                 if (lane == 0) claim = nwaves + g_add(&P.ctls[P.first_slot].jobs.v, 1u);
                 job_pending = true;
-                const double2 ab = s_bounds[p];
+                const double2 ab = P.bounds[p];   // once per job (HBM / L2)
                 const double A = ab.x, B = ab.y;
                 double* fm = L.sfm[wid];
                 auto position = [&](unsigned kk, bool& valid) -> unsigned long long {

@@ -47,7 +47,7 @@ constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM
 constexpr int GIVE_ROUNDS = 4;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
-constexpr int MAXK = 256;           // max integrals per launch
+constexpr int MAXK = 2048;          // max integrals per launch (tag: 24 bits of the pair's dt word)
 constexpr int DEFAULT_GSPLIT = 16;  // a multi-integral launch's job = the share of this many waves
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
@@ -199,7 +199,8 @@ __device__ __forceinline__ void publish_chunk(const StreamParams& P, const LdsPa
 // Per-wave accumulators of the integral currently being summed (`tag`).
 struct Acc {
     double hi, lo;                  // double-double area (aq_device.h two_sum)
-    unsigned tasks, leaves, maxd;
+    unsigned tasks, leaves, maxd;   // per lane (seeding, mixed rounds)
+    unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
 };
 
 // Flush a wave's accumulators for integral `tag`: counts into this workgroup's partial (three
@@ -208,7 +209,7 @@ struct Acc {
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all) {
     double hi = a.hi, lo = a.lo;
     wave_sum_dd(hi, lo);
-    const unsigned t = wave_sum_u(a.tasks), l = wave_sum_u(a.leaves), m = wave_max_u(a.maxd);
+    const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
         WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
         atomicAdd(&w->tasks, (unsigned long long)t);
@@ -223,19 +224,30 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     }
     a.hi = a.lo = 0.0;
     a.tasks = a.leaves = a.maxd = 0;
+    a.ut = a.ul = 0;
+    __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
 // Ring slot of monotonic ring index i (WCAP is not a power of two).
 __device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned)WCAP; }
+// Ring slot of b + k for a slot b < WCAP and k < WCAP: one subtract and one unsigned min.
+__device__ __forceinline__ unsigned ring_wrap(unsigned v) { return min(v, v - (unsigned)WCAP); }
 
 template <int FID, bool HIST, bool DIAG>
 __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
-    __shared__ double s_a[LREC], s_m[LREC], s_b[LREC], s_fa[LREC], s_fm[LREC], s_fb[LREC];
+    // one SoA block (a | m | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
+    // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds)
+    __shared__ double s_pr[6 * LREC];
     __shared__ unsigned s_dt[LREC];
+    double* const s_a = s_pr;
+    double* const s_m = s_pr + LREC;
+    double* const s_b = s_pr + 2 * LREC;
+    double* const s_fa = s_pr + 3 * LREC;
+    double* const s_fm = s_pr + 4 * LREC;
+    double* const s_fb = s_pr + 5 * LREC;
     __shared__ ExpEntry tab[128];
     __shared__ WgState S;
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
-    __shared__ double2 s_bounds[MAXK];   // {a, b} of every integral of the launch
 
     const unsigned tid = threadIdx.x;
     const unsigned lane = lane_id();
@@ -250,10 +262,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
-    if (tid < (unsigned)P.nprob && tid < (unsigned)MAXK) {
-        P.parts[(size_t)(P.first_slot + tid) * gridDim.x + blockIdx.x].cu = cu_slot();
-        s_bounds[tid] = P.bounds[tid];
-    }
+    for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
+        P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
@@ -277,7 +287,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
     }
 
-    Acc acc{0.0, 0.0, 0u, 0u, 0u};
+    Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u};
+    // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
+    for (unsigned i = lane; i < (unsigned)WCAP; i += 64) {
+        const unsigned j = base + i;
+        s_a[j] = 1.0; s_m[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
+    }
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
     Cellar* __restrict__ cel = P.cellar + w_all;
@@ -285,6 +300,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
     unsigned claim = 0;           // lane 0: the prefetched claim
     unsigned err = 0;
+    bool mixed = false;           // a round met pairs of another integral (never expected)
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
     bool counted_idle = false;
     unsigned poll_ctr = wid * (POLL_ROUNDS / NW);
@@ -346,9 +362,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             unsigned long long ci = 0;
             if constexpr (DIAG) ci = clk();
             if (counted_idle) {
-                const unsigned pt = __hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const unsigned pb = __hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int ph = __hip_atomic_load(&S.phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned pt = uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                const unsigned pb = uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                const int ph = uni(__hip_atomic_load(&S.phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
                 if (pt == pb) {
                     if (ph == 2) break;
                     __builtin_amdgcn_s_sleep(4);
@@ -357,19 +373,32 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
             }
             if (job_pending) {
-                job = __shfl(claim, 0, 64);
+                job = uni(__shfl(claim, 0, 64));
                 job_pending = false;
             }
             unsigned k = 0;
+            int ptag = 0;
             bool lead = false, seed = false;
             int phase;
             wave_lock(&S.lock, lane, lock_spins);
             {
-                const unsigned avail = S.ptop - S.pbot;
-                phase = S.phase;
+                const unsigned avail = uni(S.ptop - S.pbot);
+                phase = uni(S.phase);
                 if (avail > 0) {
                     k = min(avail, (unsigned)REFILL);
                     const unsigned pb = S.pbot;
+                    // a ring holds pairs of ONE integral (the rounds count without per-lane tags):
+                    // take the leading run of pool pairs that share the first pair's integral
+                    ptag = (int)uni(s_dt[POOL0 + (pb & (PCAP - 1))] >> 8);
+                    for (unsigned q0 = 0; q0 < k; q0 += 64) {
+                        const unsigned q = q0 + lane;
+                        const unsigned long long bad =
+                            __ballot(q < k && (int)(s_dt[POOL0 + ((pb + q) & (PCAP - 1))] >> 8) != ptag);
+                        if (bad) {
+                            k = q0 + (unsigned)__builtin_ctzll(bad);
+                            break;
+                        }
+                    }
                     for (unsigned i = lane; i < k; i += 64) copy_pair(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
                     if (lane == 0) {
                         S.pbot = pb + k;
@@ -384,7 +413,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         counted_idle = true;
                     }
                     __builtin_amdgcn_wave_barrier();
-                    if (phase == 0 && S.idle == NW) {   // every wave idle, pool empty, nothing to seed
+                    if (phase == 0 && uni(S.idle) == NW) {   // every wave idle, pool empty, nothing to seed
                         lead = true;
                         if (lane == 0) S.phase = 1;
                     }
@@ -398,6 +427,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
             }
             if (k) {
+                if (ptag != tag) {     // the ring's new integral
+                    flush_acc(P, acc, tag, lane, w_all);
+                    tag = ptag;
+                }
                 bot = 0;
                 top = k;
                 continue;
@@ -415,7 +448,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     flush_acc(P, acc, tag, lane, w_all);
                     tag = p;
                 }
-                const double2 ab = s_bounds[p];
+                const double2 ab = P.bounds[p];   // once per job (HBM / L2)
                 const double A = ab.x, B = ab.y;
                 double* fm = s_a + base;          // [nnodes + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
                 double* leafa = s_m + base;       // [nnodes]: larea + rarea of node (d,k)
@@ -620,8 +653,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     cnt = ld_wt(&P.chunks[cmd].count);
                 }
             }
-            cmd = __shfl(cmd, 0, 64);
-            cnt = __shfl(cnt, 0, 64);
+            cmd = uni(__shfl(cmd, 0, 64));
+            cnt = uni(__shfl(cnt, 0, 64));
             if (cmd < 0) {
                 wave_lock(&S.lock, lane, lock_spins);
                 if (lane == 0) S.phase = 2;
@@ -631,7 +664,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // load the chunk into the (empty) pool, take this workgroup's token back
             const Chunk* __restrict__ c = P.chunks + cmd;
             wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = S.ptop;
+            const unsigned pt = uni(S.ptop);
             for (unsigned i = lane; i < cnt; i += 64) {
                 const unsigned j = POOL0 + ((pt + i) & (PCAP - 1));
                 s_a[j] = ld_wt(&c->a[i]); s_m[j] = ld_wt(&c->m[i]); s_b[j] = ld_wt(&c->b[i]);
@@ -670,7 +703,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 continue;
             }
             wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = S.ptop;
+            const unsigned pt = uni(S.ptop);
             const bool fits = (pt - S.pbot) + 64u <= (unsigned)PCAP;
             if (fits) {
                 copy_pair(R, base + ring_slot(bot + lane), POOL0 + ((pt + lane) & (PCAP - 1)));
@@ -685,7 +718,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if (slot < P.qcap) g_add((int*)&qctl->q_tokens.v, 64);
                     spilled += 64;
                 }
-                slot = __shfl(slot, 0, 64);
+                slot = uni(__shfl(slot, 0, 64));
                 if (slot < P.qcap) {
                     const unsigned b = bot;
                     publish_chunk(P, R, slot, 64u, [&](unsigned i) { return base + ring_slot(b + i); }, lane);
@@ -701,12 +734,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         ++poll_ctr;
         // ---- feed idle sibling waves
         if ((poll_ctr % GIVE_ROUNDS) == 0 && size >= (unsigned)GIVE_MIN &&
-            __hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > 0 &&
-            __hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-                __hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) > 0 &&
+            uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
             const unsigned k = size / 2u;   // <= WCAP / 2 <= PCAP
             wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = S.ptop;
+            const unsigned pt = uni(S.ptop);
             const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
             if (fits) {
                 for (unsigned i = lane; i < k; i += 64)
@@ -733,13 +766,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 seen_head = g_ld(&qctl->q_head.v);
                 seen_tail = g_ld(&qctl->q_tail.v);
             }
-            slot = __shfl(slot, 0, 64);
+            slot = uni(__shfl(slot, 0, 64));
             if (slot != 0xffffffffu) {
                 if (slot >= P.qcap) {
                     err |= ERRB_OVERFLOW;
                 } else {
                     wave_lock(&S.lock, lane, lock_spins);
-                    const unsigned pavail = S.ptop - S.pbot;
+                    const unsigned pavail = uni(S.ptop - S.pbot);
                     unsigned k;
                     if (pavail >= (unsigned)DONATE_MIN) {
                         k = min((unsigned)CH, pavail / 2u);
@@ -788,66 +821,52 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (DIAG) c0 = clk();
         const unsigned n = min(size, 64u);
         const unsigned b0 = top - n;
+        const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
         const bool act = lane < n;
-        double pa = 1.0, pm = 1.0, pb = 1.0, pfa = 0.0, pfm = 0.0, pfb = 0.0;
-        unsigned dt = 0;
-        if (act) {
-            const unsigned j = base + ring_slot(b0 + lane);
-            pa = s_a[j]; pm = s_m[j]; pb = s_b[j]; pfa = s_fa[j]; pfm = s_fm[j]; pfb = s_fb[j]; dt = s_dt[j];
-        }
+        // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
+        const unsigned j0 = base + ring_wrap(b0s + lane);
+        const double pa = s_a[j0], pm = s_m[j0], pb = s_b[j0], pfa = s_fa[j0], pfm = s_fm[j0], pfb = s_fb[j0];
+        const unsigned dt = s_dt[j0];
         const unsigned d = dt & 255u;
-        const int rtag = (int)((dt >> 8) & 255u);
+        const int rtag = (int)(dt >> 8);
         const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
         Step st[2];
         task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st);
-        bool refine[2] = {false, false};
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (act && st[k].refine) {
-                if ((int)d + 1 >= max_depth) err |= ERRB_DEPTH;
-                else refine[k] = true;
+        // refine (:191) unless the depth cap is reached (then the task is dropped, error reported)
+        const bool ok = act && (int)d + 1 < max_depth;
+        const bool refine0 = ok && st[0].refine, refine1 = ok && st[1].refine;
+        if (act && !ok && (st[0].refine || st[1].refine)) err |= ERRB_DEPTH;
+        const bool leaf0 = act && !st[0].refine, leaf1 = act && !st[1].refine;
+        // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
+        // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
+        // counts are wave-level, the area one masked add per accepted task.
+        acc.ut += 2u * n;
+        acc.ul += (unsigned)__popcll(__ballot(leaf0)) + (unsigned)__popcll(__ballot(leaf1));
+        acc.maxd = max(acc.maxd, act ? d + 1u : 0u);
+        if (leaf0) acc.hi += st[0].larea + st[0].rarea;   // a lane's own few leaves: rounding far
+        if (leaf1) acc.hi += st[1].larea + st[1].rarea;   // below the total's ulp
+        mixed |= __ballot(act && rtag != tag) != 0ull;     // the invariant, checked (error if broken)
+        if (HIST) {
+            if (act) {
+                atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                const unsigned nl = (leaf0 ? 1u : 0u) + (leaf1 ? 1u : 0u);
+                if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
             }
-        }
-        // accounting, one pass per integral present in the round (almost always one: pairs of
-        // several integrals meet only after pool / queue moves); a new integral flushes the old
-        unsigned long long todo = __ballot(act);
-        while (todo) {
-            const int t = __shfl(rtag, (int)__builtin_ctzll(todo), 64);
-            if (t != tag) {
-                flush_acc(P, acc, tag, lane, w_all);
-                tag = t;
-                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_MIXED_ROUNDS], 1ull); }
-            }
-            const bool mine = act && rtag == t;
-            if (mine) {
-                acc.tasks += 2u;
-                acc.maxd = max(acc.maxd, d + 1u);
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    if (HIST) atomicAdd(&P.ctls[P.first_slot + t].hist[d], 1ull);
-                    if (!st[k].refine) {
-                        acc.hi += st[k].larea + st[k].rarea;   // :199 -> :149 (a lane's own few leaves:
-                                                               // rounding far below the total's ulp)
-                        ++acc.leaves;
-                        if (HIST) atomicAdd(&P.ctls[P.first_slot + t].hist[AQ_MAX_LEVELS + d], 1ull);
-                    }
-                }
-            }
-            todo &= ~__ballot(mine);
         }
         if constexpr (DIAG) c1 = clk();
         // each refining task pushes its children as one pair (:192-197)
-        const unsigned long long mask0 = __ballot(refine[0]), mask1 = __ballot(refine[1]);
+        const unsigned long long mask0 = __ballot(refine0), mask1 = __ballot(refine1);
         const unsigned cnt0 = (unsigned)__popcll(mask0);
-        const unsigned cdt = (d + 1u) | ((unsigned)rtag << 8);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (refine[k]) {
-                const unsigned pos = b0 + (k == 0 ? mbcnt(mask0) : cnt0 + mbcnt(mask1));
-                const unsigned j = base + ring_slot(pos);
-                s_a[j] = tl[k]; s_m[j] = st[k].mid; s_b[j] = tr[k];
-                s_fa[j] = tfl[k]; s_fm[j] = st[k].fmid; s_fb[j] = tfr[k]; s_dt[j] = cdt;
-            }
+        const unsigned cdt = dt + 1u;                       // depth + 1, same integral
+        if (refine0) {
+            const unsigned j = base + ring_wrap(b0s + mbcnt(mask0));
+            s_a[j] = pa; s_m[j] = st[0].mid; s_b[j] = pm;
+            s_fa[j] = pfa; s_fm[j] = st[0].fmid; s_fb[j] = pfm; s_dt[j] = cdt;
+        }
+        if (refine1) {
+            const unsigned j = base + ring_wrap(b0s + cnt0 + mbcnt(mask1));
+            s_a[j] = pm; s_m[j] = st[1].mid; s_b[j] = pb;
+            s_fa[j] = pfm; s_fm[j] = st[1].fmid; s_fb[j] = pfb; s_dt[j] = cdt;
         }
         top = b0 + cnt0 + (unsigned)__popcll(mask1);
         if constexpr (DIAG) {
@@ -863,10 +882,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned nt = 2u * n;
             if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
         }
+        __builtin_amdgcn_wave_barrier();   // reconverge before the loop latch (keeps wave state uniform)
     }
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
     flush_acc(P, acc, tag, lane, w_all);
+    if (mixed) err |= ERRB_OVERFLOW;
     const unsigned werr = wave_or_u(err);
     if (lane == 0) {
         if (werr) {

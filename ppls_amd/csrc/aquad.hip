@@ -230,10 +230,10 @@ using namespace aq;
 
 namespace {
 
-constexpr int NSLOTS = 256;
+constexpr int NSLOTS = 2048;
 constexpr int NSTAGE = 4;          // pinned bounds staging buffers
 constexpr unsigned QCAP = 16384;
-constexpr int DFS_MIN_K = 16;     // auto engine: launches of at least this many integrals run k_dfs  // HBM queue slots (16384 x 13.4 KiB = 219 MiB)
+constexpr int DFS_MIN_K = 1 << 30;   // auto engine: k_stream (measured faster); k_dfs on request
 static_assert(MAXK <= NSLOTS, "a launch's integrals need distinct slots");
 
 #define AQ_HIP(call)                                                                  \
@@ -313,6 +313,9 @@ struct aq_ctx {
     size_t front_cap = 0;
     unsigned* d_count = nullptr;
     // eval buffers
+    double* d_batch = nullptr;         // batch front end: MAXK x {area, tasks, accepted, error}
+    double* h_batch = nullptr;         // pinned, batch_cap rows
+    size_t batch_cap = 0;
     double* d_x = nullptr;
     double* d_y = nullptr;
     size_t eval_cap = 0;
@@ -596,6 +599,8 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_front[1]);
     (void)hipFree(c->d_count);
     (void)hipFree(c->d_x);
+    (void)hipFree(c->d_batch);
+    if (c->h_batch) (void)hipHostFree(c->h_batch);
     (void)hipFree(c->d_y);
     if (c->h_bounds) (void)hipHostFree(c->h_bounds);
     for (int i = 0; i < NSTAGE; ++i)
@@ -829,29 +834,51 @@ int aq_eval_cosh(aq_ctx* ctx, size_t n, const double* x, double* out) {
 int aq_integrate_batch(aq_ctx* ctx, int integrand, size_t n, const double* a, const double* b, double eps,
                        double* area, uint64_t* tasks, uint64_t* accepted) {
     // Batch front end (SURVEY config 3): MAXK integrals per persistent launch, every integral with
-    // its own slot and per-workgroup partials; launches are pipelined on the context's stream.
+    // its own slot; each launch's slots are gathered on the device into one row block that is
+    // copied back asynchronously, so launches, gathers and copies stream back to back with one
+    // host synchronisation at the end.
     if (!ctx || (n && (!a || !b))) return AQ_EINVAL;
+    if (integrand != AQ_F_COSH4 && integrand != AQ_F_SIN_RECIP) return AQ_EINVAL;
+    if (!(eps >= 0.0)) return AQ_EINVAL;
     for (size_t i = 0; i < n; ++i)
         if (!bounds_ok(a[i], b[i])) return AQ_EINVAL;
+    if (n == 0) return AQ_OK;
+    AQ_HIP(hipSetDevice(ctx->device));
+    if (!ctx->d_batch) AQ_HIP(hipMalloc(&ctx->d_batch, sizeof(double) * 4 * MAXK));
+    if (ctx->batch_cap < n) {
+        if (ctx->h_batch) AQ_HIP(hipHostFree(ctx->h_batch));
+        ctx->h_batch = nullptr;
+        AQ_HIP(hipHostMalloc(&ctx->h_batch, sizeof(double) * 4 * n, hipHostMallocDefault));
+        ctx->batch_cap = n;
+    }
     const bool hist = ctx->histograms;
     ctx->histograms = false;
     int rc = AQ_OK;
-    size_t done = 0;
-    while (done < n && rc == AQ_OK) {
+    for (size_t done = 0; done < n && rc == AQ_OK;) {
         const int m = (int)std::min<size_t>(n - done, (size_t)MAXK);
         rc = aq_integrate_many_async(ctx, integrand, m, a + done, b + done, eps, 0, 0, 1, 0);
-        for (int i = 0; i < m && rc == AQ_OK; ++i) {
-            aq_result r{};
-            rc = aq_fetch(ctx, i, &r);
-            if (rc) break;
-            if (area) area[done + i] = r.area;
-            if (tasks) tasks[done + i] = r.tasks;
-            if (accepted) accepted[done + i] = r.accepted;
+        if (rc) break;
+        rc = aq_gather_results(ctx, 0, m, ctx->d_batch);
+        if (rc) break;
+        if (hipMemcpyAsync(ctx->h_batch + 4 * done, ctx->d_batch, sizeof(double) * 4 * (size_t)m,
+                           hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) {
+            rc = AQ_EHIP;
+            break;
         }
         done += (size_t)m;
     }
     ctx->histograms = hist;
-    return rc;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == AQ_OK) rc = AQ_EHIP;
+    if (rc) return rc;
+    unsigned errbits = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const double* row = ctx->h_batch + 4 * i;
+        if (area) area[i] = row[0];
+        if (tasks) tasks[i] = (uint64_t)row[1];
+        if (accepted) accepted[i] = (uint64_t)row[2];
+        errbits |= (unsigned)row[3];
+    }
+    return err_from_bits(errbits);
 }
 
 int aq_kernel_timing(aq_ctx* ctx, int enable) {

@@ -204,18 +204,27 @@ def test_many_integrals_one_launch(ctx, oracle, trees):
         assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
 
 
-def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
+@pytest.mark.parametrize("engine", ["stream", "dfs"])
+def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden, engine):
+    """MAXK integrals with random bounds in ONE persistent launch (the bench's launch shape); the
+    first 256 against the committed golden fixture, all of them against the oracle."""
     k = ctx.max_integrals_per_launch
     a, b = oracle.batch_bounds(k)
     ctx.set_level_histograms(False)
+    ctx.set_engine(engine)
     try:
         ctx.integrate_many_async(a, b, 1e-3, first_slot=0)
         got = [ctx.fetch(i) for i in range(k)]
     finally:
         ctx.set_level_histograms(True)
-    assert [g.accepted for g in got] == batch_golden["leaves_eps1e-3_first256"][:k]
-    want = [float.fromhex(h) for h in batch_golden["area_eps1e-3_first256_hex"][:k]]
+        ctx.set_engine("auto")
+    assert [g.accepted for g in got[:256]] == batch_golden["leaves_eps1e-3_first256"]
+    want = [float.fromhex(h) for h in batch_golden["area_eps1e-3_first256_hex"]]
     assert all(abs(g.area - w) <= AREA_RTOL * abs(w) for g, w in zip(got, want))
+    oa, ot, ol = oracle.integrate_batch(a, b, 1e-3)
+    assert [g.accepted for g in got] == [int(v) for v in ol]
+    assert [g.tasks for g in got] == [int(v) for v in ot]
+    assert all(abs(g.area - w) <= AREA_RTOL * abs(w) for g, w in zip(got, oa))
 
 
 def test_many_sharded(ctx, oracle, trees):
@@ -238,6 +247,7 @@ def test_large_jobs_and_cellar(trees, monkeypatch):
     monkeypatch.setenv("AQ_GSPLIT", "8")
     c = Context(0)
     try:
+        c.set_engine("stream")
         c.set_level_histograms(False)
         c.set_diagnostics(True)
         g = trees["cosh4_eps1e-12"]
@@ -278,3 +288,37 @@ def test_back_to_back_launches_same_slots(ctx, oracle, batch_golden, trees):
     assert [int(v) for v in o[0, :, 2]] == want and [int(v) for v in o[2, :, 2]] == want
     assert (o[1, :, 2] == trees["cosh4_eps1e-3"]["leaves"]).all()
     assert (o[:, :, 3] == 0).all()
+
+
+@pytest.mark.parametrize("engine", ["stream", "dfs"])
+def test_engine_parity(ctx, oracle, trees, engine):
+    """Both persistent engines, forced: lone integrals (every golden tree), a 40-integral launch of
+    mixed bounds, and a sharded launch -- counts bit-exact, areas within 1e-12."""
+    ctx.set_engine(engine)
+    try:
+        for name in ["cosh4_eps1e-3", "cosh4_eps1e-10", "cosh4_eps1e-12", "sin_recip_eps1e-9", "cosh4_empty_interval"]:
+            g = trees[name]
+            r = ctx.integrate(_problem(g))
+            assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"]), (engine, name)
+            assert r.tasks_per_level == g["tasks_per_level"]
+            assert _area_ok(r.area, g["area_quad"])
+        a, b = oracle.batch_bounds(32)
+        a = np.concatenate([a, np.zeros(8)])
+        b = np.concatenate([b, np.full(8, 5.0)])
+        ctx.integrate_many_async(a, b, 1e-8, first_slot=100)
+        oa, ot, ol = oracle.integrate_batch(a, b, 1e-8)
+        for i in range(a.size):
+            r = ctx.fetch(100 + i, detail=True)
+            assert (r.tasks, r.accepted) == (int(ot[i]), int(ol[i])), (engine, i)
+            assert abs(r.area - oa[i]) <= AREA_RTOL * abs(oa[i])
+        g = trees["cosh4_eps1e-10"]
+        tot = [0, 0]
+        for s in range(5):   # 5 shards: the seeding's many-node path on both engines' grids
+            r = ctx.integrate_shard(_problem(g), s, 5)
+            o = oracle.integrate_shard(s, 5, G=ctx.num_workers, S=2, integrand=0, a=0.0, b=5.0, eps=1e-10)
+            assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
+            tot[0] += r.tasks
+            tot[1] += r.accepted
+        assert tot == [g["tasks"], g["leaves"]]
+    finally:
+        ctx.set_engine("auto")
