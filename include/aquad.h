@@ -123,6 +123,19 @@ int aq_gather_results(aq_ctx *ctx, int first_slot, int n, void *d_out);
 int aq_integrate_levels(aq_ctx *ctx, const aq_problem *p, aq_result *res, uint64_t *tasks_per_level,
                         uint64_t *leaves_per_level, int maxlev);
 
+/* Frontier engine over caller-owned device buffers (the multi-GPU rebalanced schedule of
+ * ppls_amd/frontier.py). A frontier is n records {l, r, F(l), F(r)} (4 doubles each, row-major) of
+ * one tree depth. aq_frontier_root writes the root record of [a, b] to d_out[0].
+ * aq_level_step enqueues one task step (aquadPartA.c:183-202) on every record of d_in: refining
+ * records append their two children to d_out (at most cap_out records; the number written lands in
+ * the device counter *d_n_out, which the call zeroes first), accepted ones add into the device
+ * accumulator d_acc[8] = {area hi, area lo (double-double), tasks, accepted, error bits, deepest
+ * level, 0, 0}; the caller zeroes d_acc once per integral. Both calls are asynchronous on the
+ * context's stream and never read device memory from the host. */
+int aq_frontier_root(aq_ctx *ctx, int integrand, double a, double b, double *d_out);
+int aq_level_step(aq_ctx *ctx, int integrand, const double *d_in, uint32_t n_in, double *d_out, uint32_t cap_out,
+                  double eps, int depth, int max_depth, uint32_t *d_n_out, double *d_acc);
+
 /* Per-level task / accepted histograms of the last aq_integrate* call (levels 0..maxlev-1). */
 int aq_level_histogram(aq_ctx *ctx, uint64_t *tasks_per_level, uint64_t *leaves_per_level, int maxlev);
 

@@ -169,6 +169,12 @@ static inline double F_eval(int integrand, int mode, double x)
 
 double aqo_F(int integrand, int mode, double x) { return F_eval(integrand, mode, x); }
 
+/* F over an array (the frontier level step's restatement, pyoracle.level_step). */
+void aqo_F_array(int integrand, int mode, long n, const double *x, double *out)
+{
+    for (long i = 0; i < n; i++) out[i] = F_eval(integrand, mode, x[i]);
+}
+
 void aqo_cosh_array(int mode, long n, const double *x, double *out)
 {
     for (long i = 0; i < n; i++) {

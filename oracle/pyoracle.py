@@ -77,6 +77,8 @@ def lib():
                                           ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.POINTER(_Res), up, up]
         L.aqo_integrate_shard.restype = ctypes.c_int
+        L.aqo_F_array.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, dp, dp]
+        L.aqo_F_array.restype = None
         L.aqo_F.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
         L.aqo_F.restype = ctypes.c_double
         L.aqo_quad_to_string.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_char_p, ctypes.c_int]
@@ -152,7 +154,13 @@ def expm1(x, mode=RESTATED_FMA):
 
 
 def F(x, integrand=COSH4, mode=RESTATED_FMA):
-    return lib().aqo_F(integrand, mode, float(x))
+    """F at a scalar (returns float) or an array (returns an array), restated glibc (aq_oracle.c)."""
+    if np.ndim(x) == 0:
+        return lib().aqo_F(integrand, mode, float(x))
+    x = np.ascontiguousarray(x, np.float64)
+    out = np.empty_like(x)
+    lib().aqo_F_array(integrand, mode, x.size, _dp(x), _dp(out))
+    return out
 
 
 def batch_bounds(n):
@@ -173,3 +181,66 @@ def integrate_batch(a, b, eps, integrand=COSH4, mode=RESTATED_FMA, maxlev=256):
     if rc != 0:
         raise RuntimeError(f"oracle aqo_integrate_batch failed rc={rc}")
     return area, tasks, leaves
+
+
+def level_step(fin, eps, depth, max_depth, integrand=COSH4, mode=RESTATED_FMA):
+    """CPU restatement of one frontier level (the HIP aq_level_step; aquadPartA.c:183-202 applied
+    to every record {l, r, F(l), F(r)} of fin, shape (n, 4)). Returns (children (m, 4), leaf areas,
+    tasks, error bits): refining records emit [l, mid] and [mid, r] (:192-197)."""
+    fin = np.asarray(fin, np.float64).reshape(-1, 4)
+    l, r, fl, fr = fin[:, 0], fin[:, 1], fin[:, 2], fin[:, 3]
+    mid = (l + r) / 2                                   # :187
+    fmid = F(mid, integrand, mode)                      # :188
+    lrarea = (fl + fr) * (r - l) / 2                    # :185
+    larea = (fl + fmid) * (mid - l) / 2                 # :189
+    rarea = (fmid + fr) * (r - mid) / 2                 # :190
+    ref = np.abs((larea + rarea) - lrarea) > eps        # :191
+    err = 0
+    if depth + 1 >= max_depth and ref.any():
+        err |= 4
+        ref = np.zeros_like(ref)
+        leaf = np.abs((larea + rarea) - lrarea) <= eps
+    else:
+        leaf = ~ref
+    kids = np.empty((2 * int(ref.sum()), 4), np.float64)
+    kids[0::2] = np.stack([l[ref], mid[ref], fl[ref], fmid[ref]], axis=1)
+    kids[1::2] = np.stack([mid[ref], r[ref], fmid[ref], fr[ref]], axis=1)
+    return kids, (larea + rarea)[leaf], fin.shape[0], err
+
+
+class FrontierStepper:
+    """Test-only stepper for ppls_amd.frontier on CPU torch tensors (gloo), backed by level_step."""
+
+    def __init__(self, integrand=COSH4, mode=RESTATED_FMA):
+        import torch
+        self.device = torch.device("cpu")
+        self.mode = mode
+
+    def root(self, integrand, a, b, out):
+        out[0, 0] = a
+        out[0, 1] = b
+        out[0, 2] = F(float(a), integrand, self.mode)
+        out[0, 3] = F(float(b), integrand, self.mode)
+
+    def step(self, integrand, fin, n_in, fout, cap, eps, depth, max_depth, nout, acc):
+        kids, leaves, tasks, err = level_step(fin[:n_in].numpy(), eps, depth, max_depth, integrand, self.mode)
+        if kids.shape[0] > cap:
+            err |= 2
+            kids = kids[:cap]
+        fout[:kids.shape[0]] = __import__("torch").from_numpy(kids)
+        nout[0] = kids.shape[0]
+        hi, lo = float(acc[0]), float(acc[1])
+        for v in leaves.tolist():
+            s = hi + v
+            bb = s - hi
+            lo += (hi - (s - bb)) + (v - bb)
+            hi = s
+        acc[0], acc[1] = hi, lo
+        acc[2] += tasks
+        acc[3] += leaves.size
+        acc[4] = float(int(acc[4]) | err)
+        if tasks:
+            acc[5] = max(float(acc[5]), depth + 1)
+
+    def sync(self):
+        pass

@@ -17,7 +17,7 @@ EXPORTS = (
     "aq_max_integrals_per_launch", "aq_integrate_many_async",
     "aq_synchronize", "aq_gather_results", "aq_integrate_levels", "aq_level_histogram", "aq_tasks_per_cu",
     "aq_integrate_batch", "aq_eval_integrand", "aq_eval_cosh", "aq_kernel_timing", "aq_kernel_time",
-    "aq_set_diagnostics", "aq_diagnostics",
+    "aq_set_diagnostics", "aq_diagnostics", "aq_frontier_root", "aq_level_step",
     "aq_print_reference",
 )
 
@@ -82,6 +82,9 @@ def load(build_if_missing=True):
         "aq_set_diagnostics": ([vp, ctypes.c_int], ctypes.c_int),
         "aq_diagnostics": ([vp, up, ctypes.c_int], ctypes.c_int),
         "aq_print_reference": ([vp, ctypes.c_double, up, ctypes.c_int], None),
+        "aq_frontier_root": ([vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, vp], ctypes.c_int),
+        "aq_level_step": ([vp, ctypes.c_int, vp, ctypes.c_uint32, vp, ctypes.c_uint32, ctypes.c_double, ctypes.c_int,
+                           ctypes.c_int, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -177,6 +177,109 @@ __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsig
     }
 }
 
+// Frontier engine step (caller-owned buffers, ppls_amd/frontier.py): one task step per record, the
+// refining records' children appended to `out` (wave-aggregated atomic), each block's accepted area
+// (double-double), task / accepted counts, error bits and deepest level written to its own partial
+// row; k_level_fold (one workgroup) folds the rows, in block order, into the caller's accumulator.
+struct LevelPart {
+    double hi, lo, tasks, leaves, err, levels, pad0, pad1;
+};
+
+template <int FID>
+__global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
+                                                    unsigned* __restrict__ n_out, unsigned cap_out, double eps,
+                                                    int depth, int max_depth, LevelPart* __restrict__ parts,
+                                                    const ExpEntry* __restrict__ gtab) {
+    __shared__ ExpEntry tab[128];
+    __shared__ double s_h[4], s_l[4];
+    __shared__ unsigned s_t[4], s_a[4], s_e[4];
+    stage_exp_table(tab, gtab);
+    __syncthreads();
+    double hi = 0.0, lo = 0.0;
+    unsigned tasks = 0, leaves = 0, err = 0;
+    const unsigned stride = gridDim.x * blockDim.x;
+    for (unsigned base = blockIdx.x * blockDim.x; base < n_in; base += stride) {
+        const unsigned i = base + threadIdx.x;
+        const bool active = i < n_in;
+        const Rec rc = active ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
+        const double x[1] = {(rc.l + rc.r) / 2};                         // :187
+        double f[1];
+        integrand_k<FID, 1>(x, f, tab);                                  // :188
+        const double mid = x[0], fmid = f[0];
+        const double lrarea = (rc.fl + rc.fr) * (rc.r - rc.l) / 2;       // :185
+        const double larea = (rc.fl + fmid) * (mid - rc.l) / 2;          // :189
+        const double rarea = (fmid + rc.fr) * (rc.r - mid) / 2;          // :190
+        const bool ref = active && fabs((larea + rarea) - lrarea) > eps; // :191
+        bool refine = false;
+        if (active) {
+            ++tasks;
+            if (!ref) {
+                dd_add(hi, lo, larea + rarea);                           // :199 -> :149
+                ++leaves;
+            } else if (depth + 1 >= max_depth) {
+                err |= ERRB_DEPTH;
+            } else {
+                refine = true;
+            }
+        }
+        const unsigned long long mask = __ballot(refine);
+        const unsigned cnt = (unsigned)__popcll(mask);
+        unsigned wbase = 0;
+        if (cnt) {
+            if (lane_id() == 0) wbase = atomicAdd(n_out, 2u * cnt);
+            wbase = __shfl(wbase, 0, 64);
+        }
+        if (refine) {
+            const unsigned pos = wbase + 2u * mbcnt(mask);
+            if (pos + 1 < cap_out) {
+                out[pos] = Rec{rc.l, mid, rc.fl, fmid};                  // [l, mid]  (:192-194)
+                out[pos + 1] = Rec{mid, rc.r, fmid, rc.fr};              // [mid, r]  (:195-197)
+            } else {
+                err |= ERRB_OVERFLOW;
+            }
+        }
+    }
+    wave_sum_dd(hi, lo);
+    const unsigned wt = wave_sum_u(tasks), wl = wave_sum_u(leaves), we = wave_or_u(err);
+    const unsigned w = threadIdx.x >> 6;
+    if (lane_id() == 0) { s_h[w] = hi; s_l[w] = lo; s_t[w] = wt; s_a[w] = wl; s_e[w] = we; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double H = 0.0, L = 0.0;
+        unsigned T = 0, A = 0, E = 0;
+        for (int k = 0; k < 4; ++k) { dd_add_dd(H, L, s_h[k], s_l[k]); T += s_t[k]; A += s_a[k]; E |= s_e[k]; }
+        LevelPart p;
+        p.hi = H; p.lo = L; p.tasks = (double)T; p.leaves = (double)A; p.err = (double)E;
+        p.levels = T ? (double)(depth + 1) : 0.0;
+        p.pad0 = p.pad1 = 0.0;
+        parts[blockIdx.x] = p;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_level_fold(const LevelPart* __restrict__ parts, int nparts,
+                                                   double* __restrict__ acc) {
+    if (threadIdx.x != 0) return;
+    double H = acc[0], L = acc[1], T = acc[2], A = acc[3], lev = acc[5];
+    unsigned E = (unsigned)acc[4];
+    for (int i = 0; i < nparts; ++i) {
+        const LevelPart& p = parts[i];
+        dd_add_dd(H, L, p.hi, p.lo);
+        T += p.tasks;
+        A += p.leaves;
+        E |= (unsigned)p.err;
+        lev = fmax(lev, p.levels);
+    }
+    acc[0] = H; acc[1] = L; acc[2] = T; acc[3] = A; acc[4] = (double)E; acc[5] = lev;
+}
+
+template <int FID>
+__global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* out, const ExpEntry* __restrict__ gtab) {
+    __shared__ ExpEntry tab[128];
+    stage_exp_table(tab, gtab);
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = Rec{a, b, integrand<FID>(a, tab), integrand<FID>(b, tab)};
+}
+
 // Gather n slots' totals into a caller device buffer as f64 [area, tasks, accepted, error] rows,
 // ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot sums the
 // slot's per-workgroup partials in a fixed order.
@@ -313,6 +416,7 @@ struct aq_ctx {
     size_t front_cap = 0;
     unsigned* d_count = nullptr;
     // eval buffers
+    LevelPart* d_lparts = nullptr;     // frontier engine: per-block partials of one level step
     double* d_batch = nullptr;         // batch front end: MAXK x {area, tasks, accepted, error}
     double* h_batch = nullptr;         // pinned, batch_cap rows
     size_t batch_cap = 0;
@@ -600,6 +704,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_count);
     (void)hipFree(c->d_x);
     (void)hipFree(c->d_batch);
+    (void)hipFree(c->d_lparts);
     if (c->h_batch) (void)hipHostFree(c->h_batch);
     (void)hipFree(c->d_y);
     if (c->h_bounds) (void)hipHostFree(c->h_bounds);
@@ -879,6 +984,42 @@ int aq_integrate_batch(aq_ctx* ctx, int integrand, size_t n, const double* a, co
         errbits |= (unsigned)row[3];
     }
     return err_from_bits(errbits);
+}
+
+int aq_frontier_root(aq_ctx* ctx, int integrand, double a, double b, double* d_out) {
+    if (!ctx || !d_out || !bounds_ok(a, b)) return AQ_EINVAL;
+    if (integrand != AQ_F_COSH4 && integrand != AQ_F_SIN_RECIP) return AQ_EINVAL;
+    AQ_HIP(hipSetDevice(ctx->device));
+    if (integrand == AQ_F_COSH4)
+        hipLaunchKernelGGL((k_frontier_root<F_COSH4>), dim3(1), dim3(64), 0, ctx->stream, a, b, (Rec*)d_out, ctx->d_tab);
+    else
+        hipLaunchKernelGGL((k_frontier_root<F_SIN_RECIP>), dim3(1), dim3(64), 0, ctx->stream, a, b, (Rec*)d_out,
+                           ctx->d_tab);
+    AQ_HIP(hipGetLastError());
+    return AQ_OK;
+}
+
+int aq_level_step(aq_ctx* ctx, int integrand, const double* d_in, uint32_t n_in, double* d_out, uint32_t cap_out,
+                  double eps, int depth, int max_depth, uint32_t* d_n_out, double* d_acc) {
+    constexpr int MAXB = 8192;   // level-step grid cap (grid-stride beyond)
+    if (!ctx || !d_n_out || !d_acc || (n_in && (!d_in || !d_out))) return AQ_EINVAL;
+    if (integrand != AQ_F_COSH4 && integrand != AQ_F_SIN_RECIP) return AQ_EINVAL;
+    if (!(eps >= 0.0) || depth < 0 || max_depth < 1 || max_depth > AQ_MAX_LEVELS - 1) return AQ_EINVAL;
+    AQ_HIP(hipSetDevice(ctx->device));
+    if (!ctx->d_lparts) AQ_HIP(hipMalloc(&ctx->d_lparts, sizeof(LevelPart) * MAXB));
+    AQ_HIP(hipMemsetAsync(d_n_out, 0, sizeof(uint32_t), ctx->stream));
+    if (n_in == 0) return AQ_OK;
+    const int grid = (int)std::min<size_t>(((size_t)n_in + 255) / 256, (size_t)MAXB);
+    if (integrand == AQ_F_COSH4)
+        hipLaunchKernelGGL((k_level_step<F_COSH4>), dim3(grid), dim3(256), 0, ctx->stream, (const Rec*)d_in, n_in,
+                           (Rec*)d_out, d_n_out, cap_out, eps, depth, max_depth, ctx->d_lparts, ctx->d_tab);
+    else
+        hipLaunchKernelGGL((k_level_step<F_SIN_RECIP>), dim3(grid), dim3(256), 0, ctx->stream, (const Rec*)d_in, n_in,
+                           (Rec*)d_out, d_n_out, cap_out, eps, depth, max_depth, ctx->d_lparts, ctx->d_tab);
+    AQ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_level_fold, dim3(1), dim3(64), 0, ctx->stream, ctx->d_lparts, grid, d_acc);
+    AQ_HIP(hipGetLastError());
+    return AQ_OK;
 }
 
 int aq_kernel_timing(aq_ctx* ctx, int enable) {

@@ -1,0 +1,216 @@
+"""Rebalanced frontier engine across GPUs (BASELINE.json north star: "frontier sizes
+are exchanged and rebalanced periodically over RCCL on xGMI").
+
+Reference: /root/reference/aquadPartA.c. The reference balances load with its farmer's bag of tasks
+(:125-173): any idle worker gets the next interval. Across GPUs the same job is done here level by
+level: every rank holds a breadth-first frontier of intervals of one tree depth in HBM, applies the
+task step (:183-202) to all of it with one HIP launch (aq_level_step, include/aquad.h), and after
+every `rebalance_every` levels the ranks
+
+  1. all-gather their frontier sizes (one int64 per rank), and
+  2. move records from ranks above the mean to ranks below it with grouped point-to-point
+     send / recv of contiguous record slices (torch.distributed P2P = RCCL over xGMI on "nccl"),
+
+so a skewed integrand (sin(1/x), SURVEY H5: 4.7x imbalance under a static partition) keeps every
+GPU busy. The run ends when the all-gathered sizes sum to zero (the farmer's `!is_empty(bag) ||
+idle_count != workers`, :166). Every decision is the reference's arithmetic on the interval's own
+endpoints, so the tree -- task and accepted counts -- is the reference's whatever the moves.
+
+The per-rank accumulators {area (double-double), tasks, accepted, error bits, deepest level} stay
+on the device; the final combine is one all-gather of them, folded on the host in double-double.
+
+Backends: the product stepper is HipStepper (the C ABI). Tests pass the oracle's CPU restatement
+(oracle/pyoracle.py: level_step) with the gloo backend to cover the multi-rank protocol on CPU.
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .aquad import AquadError, Problem, _check
+
+REC = 4  # doubles per record {l, r, F(l), F(r)}
+ERR_NAMES = {1: "on-device wait timed out", 2: "frontier capacity exceeded", 4: "maximum refinement depth reached"}
+
+
+def plan_moves(counts: List[int]) -> List[Tuple[int, int, int]]:
+    """Deterministic transfer plan (identical on every rank): (src, dst, n) moves that bring every
+    rank to floor/ceil of the mean, taking from the largest surplus first. Ranks < total % N get
+    the extra record."""
+    n = len(counts)
+    total = int(sum(counts))
+    target = [total // n + (1 if i < total % n else 0) for i in range(n)]
+    surplus = [[i, int(counts[i]) - target[i]] for i in range(n) if counts[i] > target[i]]
+    deficit = [[i, target[i] - int(counts[i])] for i in range(n) if counts[i] < target[i]]
+    surplus.sort(key=lambda e: (-e[1], e[0]))
+    deficit.sort(key=lambda e: (-e[1], e[0]))
+    moves = []
+    si = di = 0
+    while si < len(surplus) and di < len(deficit):
+        k = min(surplus[si][1], deficit[di][1])
+        moves.append((surplus[si][0], deficit[di][0], k))
+        surplus[si][1] -= k
+        deficit[di][1] -= k
+        if surplus[si][1] == 0:
+            si += 1
+        if deficit[di][1] == 0:
+            di += 1
+    return moves
+
+
+def dd_add(hi: float, lo: float, h2: float, l2: float) -> Tuple[float, float]:
+    s = hi + h2
+    bb = s - hi
+    e = (hi - (s - bb)) + (h2 - bb) + lo + l2
+    s2 = s + e
+    return s2, e - (s2 - s)
+
+
+class HipStepper:
+    """The product path: one aq_level_step launch per level on the context's stream."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        self.device = torch.device("cuda", ctx.device)
+
+    def root(self, integrand: int, a: float, b: float, out: torch.Tensor):
+        _check(self.ctx.L.aq_frontier_root(self.ctx._h, integrand, float(a), float(b), out.data_ptr()),
+               "aq_frontier_root")
+
+    def step(self, integrand, fin, n_in, fout, cap, eps, depth, max_depth, nout, acc):
+        _check(self.ctx.L.aq_level_step(self.ctx._h, integrand, fin.data_ptr(), int(n_in), fout.data_ptr(), int(cap),
+                                        float(eps), int(depth), int(max_depth), nout.data_ptr(), acc.data_ptr()),
+               "aq_level_step")
+
+    def sync(self):
+        self.ctx.synchronize()
+
+
+@dataclass
+class FrontierResult:
+    area: float
+    tasks: int
+    accepted: int
+    levels: int
+    tasks_per_rank: List[int]
+    accepted_per_rank: List[int]
+    tasks_per_level: List[int] = field(default_factory=list)
+    rebalances: int = 0
+    moved_records: int = 0
+    max_frontier: int = 0
+
+
+def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebalance_every: int = 1,
+              capacity: int = 1 << 22) -> FrontierResult:
+    """One integral over every rank of `group` (torch.distributed, initialised by the caller; a
+    single process runs without one). Collective: every rank calls it with the same arguments."""
+    problem = problem or Problem()
+    if stepper is None:
+        raise AquadError("frontier.integrate needs a stepper (HipStepper(ctx) on the GPU)")
+    if rebalance_every < 1:
+        raise AquadError("rebalance_every must be >= 1")
+    integrand = problem.integrand if isinstance(problem.integrand, int) else {"cosh4": 0, "sin_recip": 1}[problem.integrand]
+    max_depth = problem.max_depth or 96
+    distributed = dist.is_available() and dist.is_initialized()
+    rank = dist.get_rank(group) if distributed else 0
+    world = dist.get_world_size(group) if distributed else 1
+    dev = stepper.device
+    comm_dev = dev if (distributed and dist.get_backend(group) == "nccl") else torch.device("cpu")
+
+    fronts = [torch.empty((capacity, REC), dtype=torch.float64, device=dev) for _ in range(2)]
+    nout = torch.zeros(1, dtype=torch.int32, device=dev)
+    acc = torch.zeros(8, dtype=torch.float64, device=dev)
+    cur = 0
+    n = 0
+    if rank == 0:
+        stepper.root(integrand, problem.a, problem.b, fronts[cur])
+        n = 1
+    depth = 0
+    rebalances = moved = 0
+    max_front = 1
+    per_level = []
+    while True:
+        if depth >= max_depth + 1:
+            raise AquadError("frontier: maximum refinement depth reached")
+        nxt = 1 - cur
+        stepper.step(integrand, fronts[cur], n, fronts[nxt], capacity, problem.eps, depth, max_depth, nout, acc)
+        stepper.sync()
+        produced = int(nout.item())
+        if produced > capacity:
+            raise AquadError(f"frontier capacity exceeded on rank {rank}: {produced} > {capacity}")
+        per_level.append(n)
+        cur, n, depth = nxt, produced, depth + 1
+        counts = torch.tensor([n], dtype=torch.int64, device=comm_dev)
+        if world > 1:
+            gathered = [torch.zeros(1, dtype=torch.int64, device=comm_dev) for _ in range(world)]
+            dist.all_gather(gathered, counts, group=group)
+            sizes = [int(g.item()) for g in gathered]
+        else:
+            sizes = [n]
+        total = sum(sizes)
+        max_front = max(max_front, total)
+        if total == 0:
+            break
+        if world > 1 and depth % rebalance_every == 0:
+            moves = plan_moves(sizes)
+            if moves:
+                rebalances += 1
+                ops = []
+                staged = []        # (device slice, host buffer): a CPU backend (gloo) with device records
+                send_end = n
+                recv_at = n
+                for src, dst, k in moves:
+                    moved += k
+                    if src == rank:
+                        buf = fronts[cur][send_end - k:send_end]
+                        if buf.device != comm_dev:
+                            buf = buf.to(comm_dev)
+                        ops.append(dist.P2POp(dist.isend, buf, dst, group))
+                        send_end -= k
+                    elif dst == rank:
+                        if recv_at + k > capacity:
+                            raise AquadError(f"frontier capacity exceeded on rank {rank} while receiving")
+                        buf = fronts[cur][recv_at:recv_at + k]
+                        if buf.device != comm_dev:
+                            host = torch.empty((k, REC), dtype=torch.float64, device=comm_dev)
+                            staged.append((buf, host))
+                            buf = host
+                        ops.append(dist.P2POp(dist.irecv, buf, src, group))
+                        recv_at += k
+                if ops:
+                    for req in dist.batch_isend_irecv(ops):
+                        req.wait()
+                for dst_slice, host in staged:
+                    dst_slice.copy_(host)
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)   # the next level runs on the engine's own stream
+                n = send_end + (recv_at - n)      # a rank only sends or only receives
+    stepper.sync()
+    mine = acc.to(comm_dev)
+    if world > 1:
+        accs = [torch.zeros(8, dtype=torch.float64, device=comm_dev) for _ in range(world)]
+        dist.all_gather(accs, mine, group=group)
+        lv = torch.tensor(per_level, dtype=torch.int64, device=comm_dev)
+        # per-level task counts: ranks ran the same number of levels (one collective per level)
+        dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+        per_level = [int(v) for v in lv.cpu()]
+    else:
+        accs = [mine]
+    rows = [a.cpu().numpy() for a in accs]
+    hi = lo = 0.0
+    for r in rows:
+        hi, lo = dd_add(hi, lo, float(r[0]), float(r[1]))
+    err = 0
+    for r in rows:
+        err |= int(r[4])
+    if err:
+        msg = "; ".join(v for k, v in ERR_NAMES.items() if err & k)
+        raise AquadError(f"frontier: {msg}")
+    tasks = [int(r[2]) for r in rows]
+    leaves = [int(r[3]) for r in rows]
+    return FrontierResult(area=hi + lo, tasks=sum(tasks), accepted=sum(leaves), levels=int(max(r[5] for r in rows)),
+                          tasks_per_rank=tasks, accepted_per_rank=leaves, tasks_per_level=per_level,
+                          rebalances=rebalances, moved_records=moved, max_frontier=max_front)
