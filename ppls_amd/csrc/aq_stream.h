@@ -341,12 +341,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 unsigned long long cr = 0;
                 if constexpr (DIAG) cr = clk();
                 const unsigned k = min(ctop, (unsigned)REFILL), c0 = ctop - k;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's own spills have landed
+                // no wait for this wave's own spills: one wave's accesses to one address stay in
+                // order, and only this wave ever touches its cellar
                 for (unsigned q = lane; q < k; q += 64) {
                     const unsigned i = c0 + q, j = base + q;
-                    s_a[j] = ld_wt(&cel->a[i]); s_m[j] = ld_wt(&cel->m[i]); s_b[j] = ld_wt(&cel->b[i]);
-                    s_fa[j] = ld_wt(&cel->fa[i]); s_fm[j] = ld_wt(&cel->fm[i]); s_fb[j] = ld_wt(&cel->fb[i]);
-                    s_dt[j] = ld_wt(&cel->dt[i]);
+                    s_a[j] = cel->a[i]; s_m[j] = cel->m[i]; s_b[j] = cel->b[i];
+                    s_fa[j] = cel->fa[i]; s_fm[j] = cel->fm[i]; s_fb[j] = cel->fb[i];
+                    s_dt[j] = cel->dt[i];
                 }
                 ctop = c0;
                 bot = 0;
@@ -805,12 +806,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if (ctop > 0 && size <= (unsigned)PF_BELOW) {
             pf_n = min(ctop, 64u);
             ctop -= pf_n;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's own spills have landed
-            if (lane < pf_n) {
+            if (lane < pf_n) {   // (same-wave, same-address order: no wait for the spills)
                 const unsigned i = ctop + lane;
-                pf_a = ld_wt(&cel->a[i]); pf_m = ld_wt(&cel->m[i]); pf_b = ld_wt(&cel->b[i]);
-                pf_fa = ld_wt(&cel->fa[i]); pf_fm = ld_wt(&cel->fm[i]); pf_fb = ld_wt(&cel->fb[i]);
-                pf_dt = ld_wt(&cel->dt[i]);
+                pf_a = cel->a[i]; pf_m = cel->m[i]; pf_b = cel->b[i];
+                pf_fa = cel->fa[i]; pf_fm = cel->fm[i]; pf_fb = cel->fb[i];
+                pf_dt = cel->dt[i];
             }
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }
         }
