@@ -33,9 +33,15 @@
 
 namespace aq {
 
-constexpr int PT = 768;             // threads per workgroup
+#ifndef AQ_PT
+#define AQ_PT 768
+#endif
+#ifndef AQ_WCAP
+#define AQ_WCAP 208
+#endif
+constexpr int PT = AQ_PT;           // threads per workgroup
 constexpr int NW = PT / 64;         // waves (workers) per workgroup: 12, three per SIMD
-constexpr int WCAP = 208;           // per-wave LDS ring, pairs: a round pops <= 64, pushes <= 128
+constexpr int WCAP = AQ_WCAP;       // per-wave LDS ring, pairs: a round pops <= 64, pushes <= 128
 constexpr int PCAP = 256;           // per-workgroup LDS pool ring, pairs (power of two)
 constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 2752 x 52 B = 140 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
@@ -52,6 +58,10 @@ constexpr int DEFAULT_GSPLIT = 16;  // a multi-integral launch's job = the share
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches 64 cellar pairs
+#ifndef AQ_PREFETCH
+#define AQ_PREFETCH 1
+#endif
+constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch (13 VGPRs)
 
 // Queue control block (HBM ticket queue) and per-integral histogram accumulators. One per async
 // slot; it must be all-zero when a launch starts -- the host zeroes slots lazily in batches.
@@ -803,7 +813,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
 
         // ---- running low: fetch the next 64 cellar pairs now, land them next iteration
-        if (ctop > 0 && size <= (unsigned)PF_BELOW) {
+        if (PREFETCH && ctop > 0 && size <= (unsigned)PF_BELOW) {
             pf_n = min(ctop, 64u);
             ctop -= pf_n;
             if (lane < pf_n) {   // (same-wave, same-address order: no wait for the spills)
