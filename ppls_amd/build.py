@@ -24,7 +24,7 @@ HIP_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 SOURCES = [os.path.join(CSRC, "aquad.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_device.h", "aq_stream.h")] + \
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_device.h", "aq_stream.h", "aq_dfs.h")] + \
     [os.path.join(ROOT, "include", "aquad.h")]
 
 

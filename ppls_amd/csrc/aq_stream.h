@@ -37,13 +37,13 @@ namespace aq {
 #define AQ_PT 768
 #endif
 #ifndef AQ_WCAP
-#define AQ_WCAP 208
+#define AQ_WCAP 256
 #endif
 constexpr int PT = AQ_PT;           // threads per workgroup
 constexpr int NW = PT / 64;         // waves (workers) per workgroup: 12, three per SIMD
 constexpr int WCAP = AQ_WCAP;       // per-wave LDS ring, pairs: a round pops <= 64, pushes <= 128
 constexpr int PCAP = 256;           // per-workgroup LDS pool ring, pairs (power of two)
-constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 2752 x 52 B = 140 KiB
+constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 3328 x 44 B = 143 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = 256;             // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
 constexpr int S_W = 2;              // seed depth D = floor(log2 V) + S_W: 3 or 4 positions per share
@@ -93,7 +93,7 @@ struct WgPart {
 };
 
 struct Chunk {                      // SoA, one queue slot
-    double a[CH], m[CH], b[CH], fa[CH], fm[CH], fb[CH];
+    double a[CH], b[CH], fa[CH], fm[CH], fb[CH];
     unsigned dt[CH];
     unsigned count;
     unsigned pad[31];
@@ -104,7 +104,7 @@ struct Chunk {                      // SoA, one queue slot
 // the shared pool or seeds new work, so the cellar is empty whenever the wave reports idle. Only
 // the owning wave touches it (one CU, one L2), so it stays on-die.
 struct Cellar {
-    double a[CCAP], m[CCAP], b[CCAP], fa[CCAP], fm[CCAP], fb[CCAP];
+    double a[CCAP], b[CCAP], fa[CCAP], fm[CCAP], fb[CCAP];
     unsigned dt[CCAP];
 };
 
@@ -156,7 +156,6 @@ struct WgState {
 // LDS pair arrays (SoA), one per field.
 struct LdsPairs {
     double* a;
-    double* m;
     double* b;
     double* fa;
     double* fm;
@@ -185,9 +184,9 @@ __device__ __forceinline__ void wave_unlock(int* lock, unsigned lane) {
 }
 
 __device__ __forceinline__ void copy_pair(const LdsPairs& R, unsigned i, unsigned j) {
-    const double a = R.a[i], m = R.m[i], b = R.b[i], fa = R.fa[i], fm = R.fm[i], fb = R.fb[i];
+    const double a = R.a[i], b = R.b[i], fa = R.fa[i], fm = R.fm[i], fb = R.fb[i];
     const unsigned dt = R.dt[i];
-    R.a[j] = a; R.m[j] = m; R.b[j] = b; R.fa[j] = fa; R.fm[j] = fm; R.fb[j] = fb; R.dt[j] = dt;
+    R.a[j] = a; R.b[j] = b; R.fa[j] = fa; R.fm[j] = fm; R.fb[j] = fb; R.dt[j] = dt;
 }
 
 // Publish k pairs (LDS slots src(i), i < k) as HBM chunk `slot` (caller: one whole wave).
@@ -197,7 +196,7 @@ __device__ __forceinline__ void publish_chunk(const StreamParams& P, const LdsPa
     Chunk* __restrict__ c = P.chunks + slot;
     for (unsigned i = lane; i < k; i += 64) {
         const unsigned j = src(i);
-        st_wt(&c->a[i], R.a[j]); st_wt(&c->m[i], R.m[j]); st_wt(&c->b[i], R.b[j]);
+        st_wt(&c->a[i], R.a[j]); st_wt(&c->b[i], R.b[j]);
         st_wt(&c->fa[i], R.fa[j]); st_wt(&c->fm[i], R.fm[j]); st_wt(&c->fb[i], R.fb[j]);
         st_wt(&c->dt[i], R.dt[j]);
     }
@@ -238,23 +237,28 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
-// Ring slot of monotonic ring index i (WCAP is not a power of two).
+// Ring slot of monotonic ring index i.
 __device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned)WCAP; }
-// Ring slot of b + k for a slot b < WCAP and k < WCAP: one subtract and one unsigned min.
-__device__ __forceinline__ unsigned ring_wrap(unsigned v) { return min(v, v - (unsigned)WCAP); }
+// Ring slot of b + k for a slot b < WCAP and k < WCAP: one mask (power-of-two ring) or one
+// subtract and one unsigned min.
+__device__ __forceinline__ unsigned ring_wrap(unsigned v) {
+    if constexpr ((WCAP & (WCAP - 1)) == 0) return v & (unsigned)(WCAP - 1);
+    else return min(v, v - (unsigned)WCAP);
+}
 
 template <int FID, bool HIST, bool DIAG>
 __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
-    // one SoA block (a | m | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
-    // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds)
-    __shared__ double s_pr[6 * LREC];
+    // one SoA block (a | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
+    // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
+    // pair stores no midpoint: m = (a + b) / 2 is recomputed with the parent's own operands (:187),
+    // bit-identical, so a pair is 44 B and a ring holds 256 pairs.
+    __shared__ double s_pr[5 * LREC];
     __shared__ unsigned s_dt[LREC];
     double* const s_a = s_pr;
-    double* const s_m = s_pr + LREC;
-    double* const s_b = s_pr + 2 * LREC;
-    double* const s_fa = s_pr + 3 * LREC;
-    double* const s_fm = s_pr + 4 * LREC;
-    double* const s_fb = s_pr + 5 * LREC;
+    double* const s_b = s_pr + LREC;
+    double* const s_fa = s_pr + 2 * LREC;
+    double* const s_fm = s_pr + 3 * LREC;
+    double* const s_fb = s_pr + 4 * LREC;
     __shared__ ExpEntry tab[128];
     __shared__ WgState S;
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
@@ -263,7 +267,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const unsigned lane = lane_id();
     const unsigned wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps the wave state in SGPRs
     Ctl* __restrict__ qctl = P.ctls + P.first_slot;
-    const LdsPairs R{s_a, s_m, s_b, s_fa, s_fm, s_fb, s_dt};
+    const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned long long t_entry = rtc();
     stage_exp_table(tab, P.gtab);
     if (tid == 0) {
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
     for (unsigned i = lane; i < (unsigned)WCAP; i += 64) {
         const unsigned j = base + i;
-        s_a[j] = 1.0; s_m[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
+        s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
     }
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // cellar prefetch in flight: up to 64 pairs, one per lane, landed below the ring's bottom at
     // the top of the next iteration (the loads overlap one round)
     unsigned pf_n = 0;
-    double pf_a = 0, pf_m = 0, pf_b = 0, pf_fa = 0, pf_fm = 0, pf_fb = 0;
+    double pf_a = 0, pf_b = 0, pf_fa = 0, pf_fm = 0, pf_fb = 0;
     unsigned pf_dt = 0;
     const unsigned long long t0 = rtc();
     unsigned long long cl0 = 0;
@@ -338,7 +342,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             bot -= pf_n;
             if (lane < pf_n) {
                 const unsigned j = base + ring_slot(bot + lane);
-                s_a[j] = pf_a; s_m[j] = pf_m; s_b[j] = pf_b; s_fa[j] = pf_fa; s_fm[j] = pf_fm; s_fb[j] = pf_fb;
+                s_a[j] = pf_a; s_b[j] = pf_b; s_fa[j] = pf_fa; s_fm[j] = pf_fm; s_fb[j] = pf_fb;
                 s_dt[j] = pf_dt;
             }
             pf_n = 0;
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // order, and only this wave ever touches its cellar
                 for (unsigned q = lane; q < k; q += 64) {
                     const unsigned i = c0 + q, j = base + q;
-                    s_a[j] = cel->a[i]; s_m[j] = cel->m[i]; s_b[j] = cel->b[i];
+                    s_a[j] = cel->a[i]; s_b[j] = cel->b[i];
                     s_fa[j] = cel->fa[i]; s_fm[j] = cel->fm[i]; s_fb[j] = cel->fb[i];
                     s_dt[j] = cel->dt[i];
                 }
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const double2 ab = P.bounds[p];   // once per job (HBM / L2)
                 const double A = ab.x, B = ab.y;
                 double* fm = s_a + base;          // [nnodes + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
-                double* leafa = s_m + base;       // [nnodes]: larea + rarea of node (d,k)
+                double* leafa = s_b + base;       // [nnodes]: larea + rarea of node (d,k)
                 unsigned* flag = s_dt + base;     // [nnodes]: node (d,k) refines
                 auto position = [&](unsigned kk, bool& valid) -> unsigned long long {
                     const unsigned long long o = (kk & 1u) ? (unsigned long long)(V - 1 - vw) : (unsigned long long)vw;
@@ -610,7 +614,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned long long am = __ballot(alive);
                 if (alive) {
                     const unsigned j = base + mbcnt(am);
-                    s_a[j] = l; s_m[j] = mid; s_b[j] = r; s_fa[j] = fl; s_fm[j] = fmid; s_fb[j] = fr;   // :192-197
+                    s_a[j] = l; s_b[j] = r; s_fa[j] = fl; s_fm[j] = fmid; s_fb[j] = fr;   // :192-197
                     s_dt[j] = (unsigned)(D + 1) | ((unsigned)p << 8);
                 }
                 bot = 0;
@@ -678,7 +682,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned pt = uni(S.ptop);
             for (unsigned i = lane; i < cnt; i += 64) {
                 const unsigned j = POOL0 + ((pt + i) & (PCAP - 1));
-                s_a[j] = ld_wt(&c->a[i]); s_m[j] = ld_wt(&c->m[i]); s_b[j] = ld_wt(&c->b[i]);
+                s_a[j] = ld_wt(&c->a[i]); s_b[j] = ld_wt(&c->b[i]);
                 s_fa[j] = ld_wt(&c->fa[i]); s_fm[j] = ld_wt(&c->fm[i]); s_fb[j] = ld_wt(&c->fb[i]);
                 s_dt[j] = ld_wt(&c->dt[i]);
             }
@@ -706,7 +710,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if (size > (unsigned)(WCAP - 64)) {
             if (ctop + 64u <= (unsigned)CCAP) {
                 const unsigned i = ctop + lane, j = base + ring_slot(bot + lane);
-                cel->a[i] = s_a[j]; cel->m[i] = s_m[j]; cel->b[i] = s_b[j];
+                cel->a[i] = s_a[j]; cel->b[i] = s_b[j];
                 cel->fa[i] = s_fa[j]; cel->fm[i] = s_fm[j]; cel->fb[i] = s_fb[j]; cel->dt[i] = s_dt[j];
                 ctop += 64u;
                 bot += 64u;
@@ -818,7 +822,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             ctop -= pf_n;
             if (lane < pf_n) {   // (same-wave, same-address order: no wait for the spills)
                 const unsigned i = ctop + lane;
-                pf_a = cel->a[i]; pf_m = cel->m[i]; pf_b = cel->b[i];
+                pf_a = cel->a[i]; pf_b = cel->b[i];
                 pf_fa = cel->fa[i]; pf_fm = cel->fm[i]; pf_fb = cel->fb[i];
                 pf_dt = cel->dt[i];
             }
@@ -835,7 +839,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const bool act = lane < n;
         // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
         const unsigned j0 = base + ring_wrap(b0s + lane);
-        const double pa = s_a[j0], pm = s_m[j0], pb = s_b[j0], pfa = s_fa[j0], pfm = s_fm[j0], pfb = s_fb[j0];
+        const double pa = s_a[j0], pb = s_b[j0], pfa = s_fa[j0], pfm = s_fm[j0], pfb = s_fb[j0];
+        const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
         const unsigned dt = s_dt[j0];
         const unsigned d = dt & 255u;
         const int rtag = (int)(dt >> 8);
@@ -870,12 +875,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned cdt = dt + 1u;                       // depth + 1, same integral
         if (refine0) {
             const unsigned j = base + ring_wrap(b0s + mbcnt(mask0));
-            s_a[j] = pa; s_m[j] = st[0].mid; s_b[j] = pm;
+            s_a[j] = pa; s_b[j] = pm;
             s_fa[j] = pfa; s_fm[j] = st[0].fmid; s_fb[j] = pfm; s_dt[j] = cdt;
         }
         if (refine1) {
             const unsigned j = base + ring_wrap(b0s + cnt0 + mbcnt(mask1));
-            s_a[j] = pm; s_m[j] = st[1].mid; s_b[j] = pb;
+            s_a[j] = pm; s_b[j] = pb;
             s_fa[j] = pfm; s_fm[j] = st[1].fmid; s_fb[j] = pfb; s_dt[j] = cdt;
         }
         top = b0 + cnt0 + (unsigned)__popcll(mask1);
