@@ -137,6 +137,18 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
     }
 }
 
+// Constants of the exp main path that meet another constant in one FMA (gfx9 VOP3 reads at most
+// one scalar operand). A persistent kernel pins them in VGPRs once (pinned_exp_consts) instead of
+// copying them from SGPRs in every evaluation; the default instance lets the compiler choose.
+struct ExpConsts {
+    double shift = kShift, c4 = kC4, c2 = kC2;
+};
+__device__ __forceinline__ ExpConsts pinned_exp_consts() {
+    ExpConsts k;
+    asm volatile("" : "+v"(k.shift), "+v"(k.c4), "+v"(k.c2));   // opaque: kept in registers
+    return k;
+}
+
 // cosh for K independent arguments, written stage by stage so the K dependency chains interleave
 // (the main path has no branch). c[k] is exact for 0.5*ln2 <= |x[k]| < 22; the return value is a
 // lane flag set when some x[k] is outside that range, for the caller to redo with cosh_glibc.
@@ -145,7 +157,8 @@ __device__ __forceinline__ bool cosh_main_range(double x) {
     return ix >= 0x3fd62e43u && ix < 0x40360000u;
 }
 template <int K>
-__device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab) {
+__device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab,
+                                            const ExpConsts& kk) {
     double ax[K], kd[K], r[K], r2[K], tmp[K], t[K];
     uint64_t ki[K];
     ExpEntry e[K];
@@ -153,25 +166,29 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         ax[k] = fabs(x[k]);
-        kd[k] = __fma_rn(kInvLn2N, ax[k], kShift);
+        kd[k] = __fma_rn(kInvLn2N, ax[k], kk.shift);
         ki[k] = (uint64_t)__double_as_longlong(kd[k]);
         e[k] = tab[ki[k] & 127];
         out |= !cosh_main_range(x[k]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        kd[k] = kd[k] - kShift;
+        kd[k] = kd[k] - kk.shift;
         r[k] = __fma_rn(kd[k], kNegLn2loN, __fma_rn(kd[k], kNegLn2hiN, ax[k]));
         r2[k] = r[k] * r[k];
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const double tail = __longlong_as_double((long long)e[k].tail_bits);
-        tmp[k] = __fma_rn(r2[k] * r2[k], __fma_rn(r[k], kC5, kC4), __fma_rn(r2[k], __fma_rn(r[k], kC3, kC2), tail + r[k]));
+        tmp[k] = __fma_rn(r2[k] * r2[k], __fma_rn(r[k], kC5, kk.c4),
+                          __fma_rn(r2[k], __fma_rn(r[k], kC3, kk.c2), tail + r[k]));
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const double scale = __longlong_as_double((long long)(e[k].sbits + (ki[k] << 45)));
+        // e.sbits + (ki << 45): the addend's low word is zero, so only the high words add (no carry
+        // crosses the word boundary) -- one 32-bit shift-add instead of a 64-bit one
+        const uint32_t shi = (uint32_t)(e[k].sbits >> 32) + ((uint32_t)ki[k] << 13);
+        const double scale = __hiloint2double((int)shi, (int)(uint32_t)e[k].sbits);
         t[k] = __fma_rn(scale, tmp[k], scale);
     }
     double y[K], q[K];
@@ -192,10 +209,11 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 
 // F at K independent points (one round of K records per lane); every lane of the wave calls it.
 template <int FID, int K>
-__device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab) {
+__device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab,
+                                            const ExpConsts& kk = ExpConsts{}) {
     if constexpr (FID == F_COSH4) {
         double c[K];
-        const bool out = cosh_main_k<K>(x, c, tab);
+        const bool out = cosh_main_k<K>(x, c, tab, kk);
         if (__builtin_expect(__ballot(out) != 0ull, 0)) {
 #pragma unroll
             for (int k = 0; k < K; ++k)

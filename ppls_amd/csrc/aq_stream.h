@@ -333,6 +333,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         cl0 = clk();
     }
 
+    const ExpConsts kk = pinned_exp_consts();
     for (;;) {
         if (pf_n) {
             if (bot < 64u) {   // keep ring indices non-negative (slots are index % WCAP)
@@ -846,21 +847,26 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const int rtag = (int)(dt >> 8);
         const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
         Step st[2];
-        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st);
-        // refine (:191) unless the depth cap is reached (then the task is dropped, error reported)
+        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st, kk);
+        // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
+        // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
+        // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
+        const unsigned long long am = __ballot(act), dm = __ballot((int)d + 1 < max_depth);
+        const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
+        const unsigned long long okm = am & dm;
+        if (am & ~dm & (r0m | r1m)) err |= ERRB_DEPTH;
         const bool ok = act && (int)d + 1 < max_depth;
         const bool refine0 = ok && st[0].refine, refine1 = ok && st[1].refine;
-        if (act && !ok && (st[0].refine || st[1].refine)) err |= ERRB_DEPTH;
         const bool leaf0 = act && !st[0].refine, leaf1 = act && !st[1].refine;
         // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
         // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
         // counts are wave-level, the area one masked add per accepted task.
         acc.ut += 2u * n;
-        acc.ul += (unsigned)__popcll(__ballot(leaf0)) + (unsigned)__popcll(__ballot(leaf1));
+        acc.ul += (unsigned)__popcll(am & ~r0m) + (unsigned)__popcll(am & ~r1m);
         acc.maxd = max(acc.maxd, act ? d + 1u : 0u);
         if (leaf0) acc.hi += st[0].larea + st[0].rarea;   // a lane's own few leaves: rounding far
         if (leaf1) acc.hi += st[1].larea + st[1].rarea;   // below the total's ulp
-        mixed |= __ballot(act && rtag != tag) != 0ull;     // the invariant, checked (error if broken)
+        mixed |= (__ballot(rtag != tag) & am) != 0ull;     // the invariant, checked (error if broken)
         if (HIST) {
             if (act) {
                 atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
@@ -870,7 +876,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
         if constexpr (DIAG) c1 = clk();
         // each refining task pushes its children as one pair (:192-197)
-        const unsigned long long mask0 = __ballot(refine0), mask1 = __ballot(refine1);
+        const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
         const unsigned cnt0 = (unsigned)__popcll(mask0);
         const unsigned cdt = dt + 1u;                       // depth + 1, same integral
         if (refine0) {
