@@ -137,15 +137,18 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
     }
 }
 
-// Constants of the exp main path that meet another constant in one FMA (gfx9 VOP3 reads at most
-// one scalar operand). A persistent kernel pins them in VGPRs once (pinned_exp_consts) instead of
-// copying them from SGPRs in every evaluation; the default instance lets the compiler choose.
+// Constants of the exp main path. gfx9 VOP3 reads at most one scalar operand and takes no 64-bit
+// literal, so every evaluation would rebuild them (s_mov pairs, and a v_mov where two meet in one
+// FMA). A persistent kernel pins them in VGPRs once (pinned_exp_consts); the default instance lets
+// the compiler choose.
 struct ExpConsts {
     double shift = kShift, c4 = kC4, c2 = kC2;
+    double inv = kInvLn2N, hi = kNegLn2hiN, lo = kNegLn2loN, c5 = kC5, c3 = kC3;
 };
 __device__ __forceinline__ ExpConsts pinned_exp_consts() {
     ExpConsts k;
     asm volatile("" : "+v"(k.shift), "+v"(k.c4), "+v"(k.c2));   // opaque: kept in registers
+    asm volatile("" : "+v"(k.inv), "+v"(k.hi), "+v"(k.lo), "+v"(k.c5), "+v"(k.c3));
     return k;
 }
 
@@ -166,7 +169,7 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         ax[k] = fabs(x[k]);
-        kd[k] = __fma_rn(kInvLn2N, ax[k], kk.shift);
+        kd[k] = __fma_rn(kk.inv, ax[k], kk.shift);
         ki[k] = (uint64_t)__double_as_longlong(kd[k]);
         e[k] = tab[ki[k] & 127];
         out |= !cosh_main_range(x[k]);
@@ -174,14 +177,14 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         kd[k] = kd[k] - kk.shift;
-        r[k] = __fma_rn(kd[k], kNegLn2loN, __fma_rn(kd[k], kNegLn2hiN, ax[k]));
+        r[k] = __fma_rn(kd[k], kk.lo, __fma_rn(kd[k], kk.hi, ax[k]));
         r2[k] = r[k] * r[k];
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const double tail = __longlong_as_double((long long)e[k].tail_bits);
-        tmp[k] = __fma_rn(r2[k] * r2[k], __fma_rn(r[k], kC5, kk.c4),
-                          __fma_rn(r2[k], __fma_rn(r[k], kC3, kk.c2), tail + r[k]));
+        tmp[k] = __fma_rn(r2[k] * r2[k], __fma_rn(r[k], kk.c5, kk.c4),
+                          __fma_rn(r2[k], __fma_rn(r[k], kk.c3, kk.c2), tail + r[k]));
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {

@@ -181,6 +181,7 @@ __device__ __forceinline__ void wave_unlock(int* lock, unsigned lane) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) __hip_atomic_store(lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ void copy_pair(const LdsPairs& R, unsigned i, unsigned j) {
@@ -266,6 +267,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const unsigned tid = threadIdx.x;
     const unsigned lane = lane_id();
     const unsigned wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps the wave state in SGPRs
+    // one read of the workgroup id: two reads merged after a divergent loop would be a "divergent"
+    // phi, and through w_all / job every piece of wave state would follow it into VGPRs
+    const unsigned bid = __builtin_amdgcn_readfirstlane(blockIdx.x);
     Ctl* __restrict__ qctl = P.ctls + P.first_slot;
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned long long t_entry = rtc();
@@ -277,14 +281,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
     for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
-        P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].cu = cu_slot();
+        P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
     const int max_depth = P.max_depth;
     const int D = P.D;
     const unsigned W = gridDim.x * (unsigned)NW;
-    const unsigned w_all = blockIdx.x * (unsigned)NW + wid;
+    const unsigned w_all = bid * (unsigned)NW + wid;
     const unsigned shares = (unsigned)P.shares;
     const unsigned total_jobs = (unsigned)P.nprob * shares;
     const unsigned V = shares * (unsigned)P.nshards;
@@ -346,6 +350,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 s_a[j] = pf_a; s_b[j] = pf_b; s_fa[j] = pf_fa; s_fm[j] = pf_fm; s_fb[j] = pf_fb;
                 s_dt[j] = pf_dt;
             }
+            __builtin_amdgcn_wave_barrier();   // reconverge here: the ring indices stay wave-uniform
             pf_n = 0;
         }
         unsigned size = top - bot;
@@ -373,6 +378,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         atomicAdd(&s_dg[DG_C_REFILL], clk() - cr);
                     }
                 }
+                __builtin_amdgcn_wave_barrier();   // reconverge before the latch (wave state stays uniform)
                 continue;
             }
             unsigned long long ci = 0;
@@ -385,6 +391,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if (ph == 2) break;
                     __builtin_amdgcn_s_sleep(4);
                     if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_C_IDLE], clk() - ci); }
+                    __builtin_amdgcn_wave_barrier();
                     continue;
                 }
             }
@@ -420,18 +427,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         S.pbot = pb + k;
                         if (counted_idle) S.idle -= 1;
                     }
+                    __builtin_amdgcn_wave_barrier();
                     counted_idle = false;
                 } else if (job < total_jobs) {
                     seed = true;
                 } else {
                     if (!counted_idle) {
                         if (lane == 0) S.idle += 1;
+                        __builtin_amdgcn_wave_barrier();
                         counted_idle = true;
                     }
                     __builtin_amdgcn_wave_barrier();
                     if (phase == 0 && uni(S.idle) == NW) {   // every wave idle, pool empty, nothing to seed
                         lead = true;
                         if (lane == 0) S.phase = 1;
+                        __builtin_amdgcn_wave_barrier();
                     }
                 }
             }
@@ -449,6 +459,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
                 bot = 0;
                 top = k;
+                __builtin_amdgcn_wave_barrier();
                 continue;
             }
 
@@ -631,12 +642,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         atomicMax(&s_dg[DG_T_SEEDED], rtc());
                     }
                 }
+                __builtin_amdgcn_wave_barrier();
                 continue;
             }
 
             if (phase == 2) break;
             if (!lead) {
                 __builtin_amdgcn_s_sleep(4);
+                __builtin_amdgcn_wave_barrier();
                 continue;
             }
             // ---- leader: this workgroup has no work; hand its token back and wait for a chunk
@@ -703,6 +716,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     atomicAdd(&s_dg[DG_T_WAIT], rtc() - tl);
                 }
             }
+            __builtin_amdgcn_wave_barrier();
             continue;
         }
 
@@ -716,6 +730,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 ctop += 64u;
                 bot += 64u;
                 if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], 64ull); }
+                __builtin_amdgcn_wave_barrier();
                 continue;
             }
             wave_lock(&S.lock, lane, lock_spins);
@@ -744,6 +759,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_POOL_PUSH], 64ull); }
             bot += 64;
+            __builtin_amdgcn_wave_barrier();
             continue;
         }
 
@@ -766,6 +782,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_GIVE], (unsigned long long)(fits ? k : 0u)); }
             if (fits) {
                 bot += k;
+                __builtin_amdgcn_wave_barrier();
                 continue;
             }
         }
@@ -812,6 +829,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                             atomicAdd(&s_dg[DG_RECORDS_OUT], (unsigned long long)k);
                         }
                     }
+                    __builtin_amdgcn_wave_barrier();
                     continue;
                 }
             }
@@ -827,6 +845,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 pf_fa = cel->fa[i]; pf_fm = cel->fm[i]; pf_fb = cel->fb[i];
                 pf_dt = cel->dt[i];
             }
+            __builtin_amdgcn_wave_barrier();
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }
         }
 
@@ -913,9 +932,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (lane == 0) {
         if (werr) {
             for (int p = 0; p < P.nprob; ++p)
-                atomicOr(&P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].error, werr);
+                atomicOr(&P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].error, werr);
         }
-        if (spilled) atomicAdd(&P.parts[(size_t)P.first_slot * gridDim.x + blockIdx.x].spilled, spilled);
+        if (spilled) atomicAdd(&P.parts[(size_t)P.first_slot * gridDim.x + bid].spilled, spilled);
         if constexpr (DIAG) {
             atomicAdd(&s_dg[DG_LOCK_SPINS], lock_spins);
             atomicAdd(&s_dg[DG_SPILL_RECORDS], spilled);
