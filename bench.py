@@ -2,15 +2,17 @@
 """Benchmark: accepted subintervals/s (+ FP64 F-evals/s) for the reference integrand at EPSILON=1e-10.
 
 Workload (BASELINE.json configs[1]): F(x)=cosh(x)^4 (aquadPartA.c:46) over [0,5] (:47-48) at
-EPSILON=1e-10 -- 1 464 273 tasks, 732 137 accepted subintervals per integral. One step = one
-complete integral through the hot path (persistent on-device farmer, ppls_amd/csrc/aquad.hip).
-With N ranks (one process per GPU, torch.distributed backend "nccl" = RCCL) every step is sharded:
-rank r evaluates shard r of N of the SAME integral (strong scaling); the partial results of the
-K timed steps are combined with ONE all-reduce inside the timed region. Steps are pipelined
-(aq_integrate_async, no host sync between integrals); every step's counts are verified
-bit-exactly against the golden tree after timing.
+EPSILON=1e-10 -- 1 464 273 tasks, 732 137 accepted subintervals per integral. One step = one batch
+of B (default 2048) such integrals through the hot path (persistent on-device farmer,
+ppls_amd/csrc/aq_stream.h). With N ranks (one process per GPU, torch.distributed backend "nccl" =
+RCCL) every integral is sharded: rank r evaluates shard r of N of each integral (the domain split
+into subranges per GPU; strong scaling, total work fixed), and a rank packs up to N batches into
+one persistent launch so a launch holds the same work whatever N. The partial results of the K
+timed steps are combined with ONE all-reduce inside the timed region. Launches are pipelined
+(no host sync between them); every integral's counts are verified bit-exactly against the golden
+tree after timing.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--eps E] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--eps E] [--no-cpu-baseline]
 
 Prints ONE JSON line (rank 0). `value` = accepted subintervals/s over all GPUs; roofline is the
 persistent kernel's FP64 rate (38 algorithmic FLOP per task) over its HIP-event
@@ -85,14 +87,13 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8192)
-    ap.add_argument("--warmup", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=8, help="timed batches")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed batches")
+    ap.add_argument("--batch", type=int, default=2048, help="integrals per step")
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true",
                     help="skip the one-integral-per-launch latency probe (profiling runs: every dispatch is K-wide)")
-    ap.add_argument("--per-launch", type=int, default=2048,
-                    help="integrals per persistent launch (1 = one launch per integral)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,10 +112,26 @@ def main():
     import torch.distributed as dist
     from ppls_amd import Context, Problem
 
-    torch.cuda.set_device(local_rank)
+    # BENCH_SHARED_GPU=1 rehearses the N-rank path on a one-GPU box: every rank on device 0, the
+    # collectives over gloo (RCCL needs one GPU per rank). Never set by the driver.
+    shared = os.environ.get("BENCH_SHARED_GPU") == "1"
+    dev = 0 if shared else local_rank
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    ctx = Context(local_rank)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    coll = "cpu" if shared else "cuda"
+
+    def all_reduce(t, op):
+        if world > 1:
+            h = t.to(coll)
+            dist.all_reduce(h, op=op)
+            if h is not t:
+                t.copy_(h)
+
+    ctx = Context(dev)
     ctx.set_level_histograms(False)
     problem = Problem(eps=args.eps)
     nslots = ctx.async_slots
@@ -123,10 +140,23 @@ def main():
         if world > 1:
             dist.barrier()
 
-    kmax = min(ctx.max_integrals_per_launch, nslots, args.per_launch)
+    B = args.batch
+    if B < 1 or B > min(ctx.max_integrals_per_launch, nslots):
+        raise SystemExit(f"--batch must be in [1, {min(ctx.max_integrals_per_launch, nslots)}]")
+    # batches per launch: N of them (each rank holds 1/N of every integral), within the slot budget
+    lb = max(1, min(world, min(ctx.max_integrals_per_launch, nslots) // B))
 
     def launch(m):
         # m integrals of the workload in one persistent launch (slots 0..m-1), this rank's shard
+        if shared and world > 1:
+            # rehearsal: persistent grids need the whole GPU, so the ranks sharing it take turns
+            for r in range(world):
+                if r == rank:
+                    ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank,
+                                             nshards=world)
+                    ctx.synchronize()
+                dist.barrier()
+            return
         ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank, nshards=world)
 
     # single-integral latency (one integral per launch), reported beside the throughput
@@ -140,12 +170,16 @@ def main():
         ctx.kernel_timing(False)
 
     # warmup (also validates)
-    for _ in range(max(1, args.warmup // kmax)):
-        launch(kmax)
+    w = 0
+    while w < max(1, args.warmup):
+        m = min(max(1, args.warmup) - w, lb)
+        launch(m * B)
+        w += m
     ctx.synchronize()
 
     K = args.steps
-    totals = torch.zeros((K, 4), dtype=torch.float64, device="cuda")
+    n_int = K * B
+    totals = torch.zeros((n_int, 4), dtype=torch.float64, device="cuda")
     ctx.kernel_timing(True)
     barrier()
     torch.cuda.synchronize()
@@ -154,13 +188,12 @@ def main():
     while done < K:
         # launches queue back to back on the context's stream: each gathers its slots' results into
         # its rows of `totals` (device memory), and the next launch re-zeroes the slots after that
-        m = min(K - done, kmax)
-        launch(m)
-        ctx.gather_results(0, m, totals.data_ptr() + done * 4 * totals.element_size())
+        m = min(K - done, lb)
+        launch(m * B)
+        ctx.gather_results(0, m * B, totals.data_ptr() + done * B * 4 * totals.element_size())
         done += m
     ctx.synchronize()
-    if world > 1:
-        dist.all_reduce(totals, op=dist.ReduceOp.SUM)   # shard partials -> whole integrals
+    all_reduce(totals, dist.ReduceOp.SUM)   # shard partials -> whole integrals
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -170,11 +203,11 @@ def main():
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        all_reduce(tt, dist.ReduceOp.MAX)
         elapsed, kern_avg_ms = float(tt[0]), float(tt[1])
     else:
         kern_avg_ms = kern_ms / max(launches, 1)
-    per_launch = K / max(launches, 1)
+    per_launch = n_int / max(launches, 1)
 
     # verify every timed step against the golden tree
     tot = totals.cpu().numpy()
@@ -184,7 +217,7 @@ def main():
         ok = ok and bool((tot[:, 1] == tg).all() and (tot[:, 2] == lg).all())
     accepted_total = float(tot[:, 2].sum())
     tasks_total = float(tot[:, 1].sum())
-    f_evals = tasks_total + 2 * K   # algorithmic F evaluations: 1 per task + F(A), F(B) per integral
+    f_evals = tasks_total + 2 * n_int   # algorithmic F evaluations: 1 per task + F(A), F(B) per integral
 
     # this rank's share of the tasks per launch, for the roofline of its kernel
     mine = ctx.fetch(0)
@@ -206,10 +239,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (analytic integrand, no dataset)",
-            "config": {"workload": "cosh4 on [0,5], EPSILON=%g, one integral per step (BASELINE configs[1])" % args.eps,
+            "config": {"workload": "cosh4 on [0,5], EPSILON=%g (BASELINE configs[1]); one step = a batch of %d "
+                                   "such integrals, each sharded over the GPUs" % (args.eps, B),
                        "integrand": "cosh(x)^4 (aquadPartA.c:46)", "a": 0.0, "b": 5.0, "eps": args.eps,
                        "tasks_per_integral": int(tot[0, 1]), "accepted_per_integral": int(tot[0, 2]),
                        "parallelism": f"shard{world}" if world > 1 else "single-gpu",
+                       "integrals_per_step": B,
                        "integrals_per_launch": per_launch,
                        "workgroups_per_gpu": ctx.num_cus},
             "single_integral_kernel_us": single_ms * 1e3 / single_n if single_n else None,

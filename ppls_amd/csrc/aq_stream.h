@@ -53,7 +53,7 @@ constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM
 constexpr int GIVE_ROUNDS = 4;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
-constexpr int MAXK = 2048;          // max integrals per launch (tag: 24 bits of the pair's dt word)
+constexpr int MAXK = 16384;         // max integrals per launch (tag: 24 bits of the pair's dt word)
 constexpr int DEFAULT_GSPLIT = 32;  // a multi-integral launch's job = the share of this many waves
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar

@@ -333,7 +333,7 @@ using namespace aq;
 
 namespace {
 
-constexpr int NSLOTS = 2048;
+constexpr int NSLOTS = 16384;
 constexpr int NSTAGE = 4;          // pinned bounds staging buffers
 constexpr unsigned QCAP = 16384;
 constexpr int DFS_MIN_K = 1 << 30;   // auto engine: k_stream (measured faster); k_dfs on request
@@ -493,8 +493,11 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.shard = shard;
     P.nshards = nshards;
     // jobs: one integral is split into one share per wave (the partition the oracle restates); a
-    // multi-integral launch uses gsplit-times larger shares, so one seeding pass feeds more rounds
-    int gs = k >= 16 ? DEFAULT_GSPLIT : 1;
+    // multi-integral launch uses gsplit-times larger shares, so one seeding pass feeds more rounds.
+    // A shard of N holds 1/N of each integral: its shares are N times fewer, so a job (and its
+    // seeding overhead) stays the same size whatever N (strong scaling).
+    int gs = k >= 16 ? DEFAULT_GSPLIT * std::max(1, nshards) : 1;
+    gs = std::min(gs, W);
     if (ctx->gsplit_env > 0) gs = ctx->gsplit_env;
     while (gs > 1 && W % gs != 0) gs >>= 1;
     P.shares = W / gs;
