@@ -55,6 +55,7 @@ constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers ne
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr int MAXK = 16384;         // max integrals per launch (tag: 24 bits of the pair's dt word)
 constexpr int DEFAULT_GSPLIT = 32;  // a multi-integral launch's job = the share of this many waves
+constexpr unsigned TASKS_PER_JOB = 16384;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches 64 cellar pairs
@@ -108,6 +109,15 @@ struct Cellar {
     unsigned dt[CCAP];
 };
 
+// Launch-to-launch job-size hint (one per context): every workgroup adds the tasks it ran, the last
+// one to exit turns the mean per integral into the next adaptive launch's shares per integral
+// (about TASKS_PER_JOB tasks per job) and clears the sums.
+struct alignas(128) LaunchHint {
+    unsigned long long tasks;
+    unsigned exits;
+    unsigned shares_next;   // 0: no hint yet (the launch uses StreamParams::shares)
+};
+
 struct StreamParams {
     const double2* bounds;          // [nprob] {a, b} per integral
     int nprob;
@@ -130,6 +140,8 @@ struct StreamParams {
     const ExpEntry* gtab;
     double2* stk;                   // k_dfs: per-lane DFS stacks [wave][SDEPTH][64] {x, F(x)}
     unsigned wstride;               // warea entries per slot (>= waves of any engine's grid)
+    LaunchHint* hint;
+    int adaptive;                   // take shares per integral from hint->shares_next when set
 };
 
 // Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
@@ -150,7 +162,8 @@ struct WgState {
     int idle;            // waves with nothing left (no pairs, pool empty, nothing to seed)
     int phase;           // 0 running, 1 a leader wave is at the HBM queue, 2 exit
     int busy_token;      // the workgroup holds one token of the HBM-queue protocol
-    int pad[2];
+    unsigned exited;     // waves past the loop (adaptive launches)
+    unsigned long long tasks;   // tasks this workgroup ran (adaptive launches)
 };
 
 // LDS pair arrays (SoA), one per field.
@@ -216,11 +229,13 @@ struct Acc {
 // Flush a wave's accumulators for integral `tag`: counts into this workgroup's partial (three
 // uncontended integer atomics), the double-double area into the wave's own partial (a plain
 // read-modify-write: no other wave touches it), and reset them.
-__device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all) {
+__device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all,
+                                          unsigned long long* wg_tasks) {
     double hi = a.hi, lo = a.lo;
     wave_sum_dd(hi, lo);
     const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
+        atomicAdd(wg_tasks, (unsigned long long)t);
         WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
         atomicAdd(&w->tasks, (unsigned long long)t);
         atomicAdd(&w->leaves, (unsigned long long)l);
@@ -276,6 +291,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     stage_exp_table(tab, P.gtab);
     if (tid == 0) {
         S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1;
+        S.exited = 0; S.tasks = 0;
     }
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
@@ -286,10 +302,18 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
     const double eps = P.eps;
     const int max_depth = P.max_depth;
-    const int D = P.D;
+    // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
+    unsigned shares = (unsigned)P.shares;
+    int D = P.D;
+    if (P.adaptive) {
+        const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (h) {
+            shares = h;
+            D = 63 - __builtin_clzll((unsigned long long)h * (unsigned long long)P.nshards) + S_W;
+        }
+    }
     const unsigned W = gridDim.x * (unsigned)NW;
     const unsigned w_all = bid * (unsigned)NW + wid;
-    const unsigned shares = (unsigned)P.shares;
     const unsigned total_jobs = (unsigned)P.nprob * shares;
     const unsigned V = shares * (unsigned)P.nshards;
     const unsigned long long npos_total = 1ull << D;
@@ -454,7 +478,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             if (k) {
                 if (ptag != tag) {     // the ring's new integral
-                    flush_acc(P, acc, tag, lane, w_all);
+                    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
                     tag = ptag;
                 }
                 bot = 0;
@@ -472,7 +496,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (lane == 0) claim = W + g_add(&qctl->jobs.v, 1u);   // next job: latency hides behind this one
                 job_pending = true;
                 if (p != tag) {
-                    flush_acc(P, acc, tag, lane, w_all);
+                    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
                     tag = p;
                 }
                 const double2 ab = P.bounds[p];   // once per job (HBM / L2)
@@ -926,7 +950,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     }
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
-    flush_acc(P, acc, tag, lane, w_all);
+    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
     if (mixed) err |= ERRB_OVERFLOW;
     const unsigned werr = wave_or_u(err);
     if (lane == 0) {
@@ -939,6 +963,22 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             atomicAdd(&s_dg[DG_LOCK_SPINS], lock_spins);
             atomicAdd(&s_dg[DG_SPILL_RECORDS], spilled);
             atomicAdd(&s_dg[DG_C_LOOP], clk() - cl0);
+        }
+        // job-size hint for the next adaptive launch: the last wave of each workgroup adds the
+        // workgroup's tasks, the last workgroup sets shares per integral for ~TASKS_PER_JOB per job
+        if (P.adaptive && atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u) {
+            const unsigned long long wt = __hip_atomic_load(&S.tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&P.hint->tasks, wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned g = __hip_atomic_fetch_add(&P.hint->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (g == gridDim.x - 1u) {
+                const unsigned long long tot = __hip_atomic_load(&P.hint->tasks, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long per = tot / (unsigned long long)P.nprob;   // tasks per integral (shard)
+                unsigned long long sh = (per + TASKS_PER_JOB / 2) / TASKS_PER_JOB;
+                sh = sh < 1ull ? 1ull : (sh > (unsigned long long)W ? (unsigned long long)W : sh);
+                __hip_atomic_store(&P.hint->shares_next, (unsigned)sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&P.hint->tasks, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&P.hint->exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     if constexpr (DIAG) {

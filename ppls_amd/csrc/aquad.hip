@@ -409,6 +409,7 @@ struct aq_ctx {
     int engine = AQ_ENGINE_AUTO;       // aq_set_engine
     int wstride = 0;                   // warea entries per slot: max waves of either engine's grid
     double2* d_stk = nullptr;          // k_dfs lane stacks, grid * DW * SDEPTH * 64 entries
+    LaunchHint* d_hint = nullptr;      // job-size hint carried from launch to launch
     int gsplit_env = 0;                // AQ_GSPLIT: waves per job of a multi-integral launch (0 = default)
     // level path
     DevResults* d_lres = nullptr;
@@ -516,6 +517,9 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.gtab = ctx->d_tab;
     P.stk = ctx->d_stk;
     P.wstride = (unsigned)ctx->wstride;
+    P.hint = ctx->d_hint;
+    // multi-integral stream launches size their jobs from the previous launch's tasks per integral
+    P.adaptive = (!dfs && k >= 16 && ctx->gsplit_env <= 0) ? 1 : 0;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (ctx->timing) {
         if (!ctx->ev_free.empty()) {
@@ -666,6 +670,8 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipHostMalloc(&c->h_warea, sizeof(double2) * (size_t)c->wstride, hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_stk, sizeof(double2) * (size_t)c->grid * DW * SDEPTH * 64));
     AQ_HIP(hipMalloc(&c->d_bounds, sizeof(double2) * NSLOTS));
+    AQ_HIP(hipMalloc(&c->d_hint, sizeof(LaunchHint)));
+    AQ_HIP(hipMemset(c->d_hint, 0, sizeof(LaunchHint)));
     AQ_HIP(hipHostMalloc(&c->h_bounds, sizeof(double2) * NSLOTS * NSTAGE, hipHostMallocDefault));
     for (int i = 0; i < NSTAGE; ++i) {
         AQ_HIP(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
@@ -696,6 +702,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     (void)hipFree(c->d_parts);
     (void)hipFree(c->d_warea);
     (void)hipFree(c->d_bounds);
+    (void)hipFree(c->d_hint);
     (void)hipFree(c->d_chunks);
     (void)hipFree(c->d_cellar);
     (void)hipFree(c->d_stk);
