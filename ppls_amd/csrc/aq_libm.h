@@ -13,6 +13,9 @@
 // The 2 KiB exp table lives in LDS (one ds_read_b128 per lookup); kernels stage it at entry
 // with aq_stage_exp_table().
 #pragma once
+#ifndef AQ_PIN_CONSTS
+#define AQ_PIN_CONSTS 1
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -147,8 +150,10 @@ struct ExpConsts {
 };
 __device__ __forceinline__ ExpConsts pinned_exp_consts() {
     ExpConsts k;
+#if AQ_PIN_CONSTS
     asm volatile("" : "+v"(k.shift), "+v"(k.c4), "+v"(k.c2));   // opaque: kept in registers
     asm volatile("" : "+v"(k.inv), "+v"(k.hi), "+v"(k.lo), "+v"(k.c5), "+v"(k.c3));
+#endif
     return k;
 }
 

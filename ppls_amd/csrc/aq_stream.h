@@ -55,7 +55,7 @@ constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers ne
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr int MAXK = 16384;         // max integrals per launch (tag: 24 bits of the pair's dt word)
 constexpr int DEFAULT_GSPLIT = 32;  // a multi-integral launch's job = the share of this many waves
-constexpr unsigned TASKS_PER_JOB = 16384;   // adaptive job size: a job holds about this many tasks
+constexpr unsigned TASKS_PER_JOB = 15000;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches 64 cellar pairs
