@@ -141,7 +141,7 @@ struct StreamParams {
     double2* stk;                   // k_dfs: per-lane DFS stacks [wave][SDEPTH][64] {x, F(x)}
     unsigned wstride;               // warea entries per slot (>= waves of any engine's grid)
     LaunchHint* hint;
-    int adaptive;                   // take shares per integral from hint->shares_next when set
+    int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
 };
 
 // Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
     unsigned shares = (unsigned)P.shares;
     int D = P.D;
-    if (P.adaptive) {
+    if (P.adaptive & 1) {
         const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
             shares = h;
@@ -966,7 +966,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
         // job-size hint for the next adaptive launch: the last wave of each workgroup adds the
         // workgroup's tasks, the last workgroup sets shares per integral for ~TASKS_PER_JOB per job
-        if (P.adaptive && atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u) {
+        if ((P.adaptive & 2) && atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u) {
             const unsigned long long wt = __hip_atomic_load(&S.tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&P.hint->tasks, wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned g = __hip_atomic_fetch_add(&P.hint->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);

@@ -410,6 +410,9 @@ struct aq_ctx {
     int wstride = 0;                   // warea entries per slot: max waves of either engine's grid
     double2* d_stk = nullptr;          // k_dfs lane stacks, grid * DW * SDEPTH * 64 entries
     LaunchHint* d_hint = nullptr;      // job-size hint carried from launch to launch
+    bool hint_valid = false;           // the workload the hint was measured on
+    int hint_fid = -1, hint_nshards = 0;
+    double hint_eps = 0.0;
     int gsplit_env = 0;                // AQ_GSPLIT: waves per job of a multi-integral launch (0 = default)
     // level path
     DevResults* d_lres = nullptr;
@@ -518,8 +521,19 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.stk = ctx->d_stk;
     P.wstride = (unsigned)ctx->wstride;
     P.hint = ctx->d_hint;
-    // multi-integral stream launches size their jobs from the previous launch's tasks per integral
-    P.adaptive = (!dfs && k >= 16 && ctx->gsplit_env <= 0) ? 1 : 0;
+    // multi-integral stream launches size their jobs from the previous launch's tasks per integral,
+    // when that launch integrated the same integrand at the same tolerance over the same sharding
+    // (a context that switches workload starts from the default shares and a fresh hint)
+    P.adaptive = 0;
+    if (!dfs && k >= 16 && ctx->gsplit_env <= 0) {
+        const bool same = ctx->hint_valid && ctx->hint_fid == FID && ctx->hint_eps == eps &&
+                          ctx->hint_nshards == nshards;
+        P.adaptive = same ? 3 : 2;
+        ctx->hint_valid = true;
+        ctx->hint_fid = FID;
+        ctx->hint_eps = eps;
+        ctx->hint_nshards = nshards;
+    }
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (ctx->timing) {
         if (!ctx->ev_free.empty()) {
