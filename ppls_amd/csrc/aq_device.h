@@ -107,6 +107,18 @@ __host__ __device__ __forceinline__ void dd_add_dd(double& hi, double& lo, doubl
     e += lo + l2;
     two_sum(s, e, hi, lo);
 }
+// acc += v on the lanes of `mask` only: one exec-masked v_add_f64 instead of an add and a 64-bit
+// select (two v_cndmask) per lane; lanes outside the mask keep their value.
+__device__ __forceinline__ void masked_add(double& acc, double v, unsigned long long mask) {
+    unsigned long long saved;
+    asm("s_and_saveexec_b64 %1, %3\n\t"
+        "v_add_f64 %0, %0, %2\n\t"
+        "s_mov_b64 exec, %1"
+        : "+v"(acc), "=&s"(saved)
+        : "v"(v), "s"(mask)
+        : "scc");
+}
+
 __device__ __forceinline__ void wave_sum_dd(double& hi, double& lo) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

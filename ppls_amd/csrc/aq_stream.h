@@ -904,11 +904,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
         // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
         // counts are wave-level, the area one masked add per accepted task.
+        const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
         acc.ut += 2u * n;
-        acc.ul += (unsigned)__popcll(am & ~r0m) + (unsigned)__popcll(am & ~r1m);
+        acc.ul += (unsigned)__popcll(l0m) + (unsigned)__popcll(l1m);
         acc.maxd = max(acc.maxd, act ? d + 1u : 0u);
-        if (leaf0) acc.hi += st[0].larea + st[0].rarea;   // a lane's own few leaves: rounding far
-        if (leaf1) acc.hi += st[1].larea + st[1].rarea;   // below the total's ulp
+        // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
+        masked_add(acc.hi, st[0].larea + st[0].rarea, l0m);
+        masked_add(acc.hi, st[1].larea + st[1].rarea, l1m);
         mixed |= (__ballot(rtag != tag) & am) != 0ull;     // the invariant, checked (error if broken)
         if (HIST) {
             if (act) {

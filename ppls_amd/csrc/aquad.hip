@@ -522,10 +522,12 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.wstride = (unsigned)ctx->wstride;
     P.hint = ctx->d_hint;
     // multi-integral stream launches size their jobs from the previous launch's tasks per integral,
-    // when that launch integrated the same integrand at the same tolerance over the same sharding
-    // (a context that switches workload starts from the default shares and a fresh hint)
+    // when that launch integrated the same integrand at the same tolerance (a context that switches
+    // workload starts from the default shares and a fresh hint). Not for shards: every shard of an
+    // integral must use the same partition (shares, seed depth), and each rank's hint would come
+    // from its own, slightly different, share of the work.
     P.adaptive = 0;
-    if (!dfs && k >= 16 && ctx->gsplit_env <= 0) {
+    if (!dfs && k >= 16 && ctx->gsplit_env <= 0 && nshards == 1) {
         const bool same = ctx->hint_valid && ctx->hint_fid == FID && ctx->hint_eps == eps &&
                           ctx->hint_nshards == nshards;
         P.adaptive = same ? 3 : 2;

@@ -322,3 +322,32 @@ def test_engine_parity(ctx, oracle, trees, engine):
         assert tot == [g["tasks"], g["leaves"]]
     finally:
         ctx.set_engine("auto")
+
+
+def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
+    """Multi-integral launches size their jobs from the previous launch of the same workload (a
+    device-side hint); switching workload (tiny random trees <-> the eps=1e-10 tree, sharded or
+    not) changes the shares per integral, never the counts."""
+    g10 = trees["cosh4_eps1e-10"]
+    a, b = oracle.batch_bounds(64)
+    oa, ot, ol = oracle.integrate_batch(a, b, 1e-3)
+    ctx.set_level_histograms(False)
+    try:
+        for phase in ["big", "big", "small", "small", "big", "shard", "shard", "big"]:
+            if phase == "big":
+                ctx.integrate_many_async(np.zeros(64), np.full(64, 5.0), 1e-10, first_slot=0)
+                rs = [ctx.fetch(i) for i in range(64)]
+                assert all((r.tasks, r.accepted) == (g10["tasks"], g10["leaves"]) for r in rs), phase
+                assert all(_area_ok(r.area, g10["area_quad"]) for r in rs)
+            elif phase == "small":
+                ctx.integrate_many_async(a, b, 1e-3, first_slot=0)
+                rs = [ctx.fetch(i) for i in range(64)]
+                assert [(r.tasks, r.accepted) for r in rs] == [(int(t), int(l)) for t, l in zip(ot, ol)]
+            else:
+                tot = np.zeros((64, 2), np.int64)
+                for s in range(2):
+                    ctx.integrate_many_async(np.zeros(64), np.full(64, 5.0), 1e-10, first_slot=0, shard=s, nshards=2)
+                    tot += np.array([(r.tasks, r.accepted) for r in (ctx.fetch(i) for i in range(64))], np.int64)
+                assert (tot == np.array([g10["tasks"], g10["leaves"]])).all()
+    finally:
+        ctx.set_level_histograms(True)
