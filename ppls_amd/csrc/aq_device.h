@@ -69,11 +69,11 @@ __device__ __forceinline__ Step task_step(double l, double r, double fl, double 
 template <int FID, int K>
 __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (&r)[K], const double (&fl)[K],
                                             const double (&fr)[K], double eps, const ExpEntry* __restrict__ tab,
-                                            Step (&s)[K], const ExpConsts& kk = ExpConsts{}) {
+                                            Step (&s)[K], const ExpConsts& kk = ExpConsts{}, int range_hint = -1) {
     double mid[K], fmid[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) mid[k] = (l[k] + r[k]) / 2;   // :187
-    integrand_k<FID, K>(mid, fmid, tab, kk);                   // :188
+    integrand_k<FID, K>(mid, fmid, tab, kk, range_hint);       // :188
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const double lrarea = (fl[k] + fr[k]) * (r[k] - l[k]) / 2;   // :185

@@ -164,7 +164,7 @@ __device__ __forceinline__ bool cosh_main_range(double x) {
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
     return ix >= 0x3fd62e43u && ix < 0x40360000u;
 }
-template <int K>
+template <int K, bool CHECK = true>
 __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab,
                                             const ExpConsts& kk) {
     double ax[K], kd[K], r[K], r2[K], tmp[K], t[K];
@@ -177,7 +177,7 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
         kd[k] = __fma_rn(kk.inv, ax[k], kk.shift);
         ki[k] = (uint64_t)__double_as_longlong(kd[k]);
         e[k] = tab[ki[k] & 127];
-        out |= !cosh_main_range(x[k]);
+        if (CHECK) out |= !cosh_main_range(x[k]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -216,12 +216,27 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 }
 
 // F at K independent points (one round of K records per lane); every lane of the wave calls it.
+// A lane whose K points all lie in one interval [lo, hi] may pass range_hint = cosh_main_span(lo,
+// hi) (one test for the K points); -1 tests every point.
+__device__ __forceinline__ bool cosh_main_span(double lo, double hi) {
+    // lo >= 0 and both ends in the main range: every point between has a hi word between theirs
+    // (the word is monotonic for x >= 0), so glibc takes the exp path for all of them. Negative lo
+    // fails the unsigned test and goes to the per-point path.
+    constexpr uint32_t c0 = 0x3fd62e43u, span = 0x40360000u - 0x3fd62e43u;
+    return (hi_word(lo) - c0 < span) && (hi_word(hi) - c0 < span);
+}
 template <int FID, int K>
 __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab,
-                                            const ExpConsts& kk = ExpConsts{}) {
+                                            const ExpConsts& kk = ExpConsts{}, int range_hint = -1) {
     if constexpr (FID == F_COSH4) {
         double c[K];
-        const bool out = cosh_main_k<K>(x, c, tab, kk);
+        bool out;
+        if (range_hint >= 0) {
+            cosh_main_k<K, false>(x, c, tab, kk);
+            out = range_hint == 0;
+        } else {
+            out = cosh_main_k<K>(x, c, tab, kk);
+        }
         if (__builtin_expect(__ballot(out) != 0ull, 0)) {
 #pragma unroll
             for (int k = 0; k < K; ++k)

@@ -890,7 +890,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const int rtag = (int)(dt >> 8);
         const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
         Step st[2];
-        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st, kk);
+        // both midpoints lie in [pa, pb]: one range test for the pair
+        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st, kk, FID == F_COSH4 ? (int)cosh_main_span(pa, pb) : -1);
         // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
         // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
         // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
