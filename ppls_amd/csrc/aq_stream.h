@@ -46,7 +46,10 @@ constexpr int PCAP = 256;           // per-workgroup LDS pool ring, pairs (power
 constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 3328 x 44 B = 143 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = 256;             // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
-constexpr int S_W = 2;              // seed depth D = floor(log2 V) + S_W: 3 or 4 positions per share
+#ifndef AQ_S_W
+#define AQ_S_W 2
+#endif
+constexpr int S_W = AQ_S_W;              // seed depth D = floor(log2 V) + S_W: 3 or 4 positions per share
 constexpr int GIVE_MIN = 96;        // a busy wave feeds the pool for idle siblings only above this size
 constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup donates from its pool
 constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
@@ -493,8 +496,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if constexpr (DIAG) cs = clk();
                 const int p = (int)(job / shares);
                 const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
-                if (lane == 0) claim = W + g_add(&qctl->jobs.v, 1u);   // next job: latency hides behind this one
-                job_pending = true;
+                if (total_jobs > W) {
+                    if (lane == 0) claim = W + g_add(&qctl->jobs.v, 1u);   // next job: latency hides behind this one
+                    job_pending = true;
+                } else {
+                    // every job was handed out at launch (job = w_all): no claim, so a lone integral's
+                    // 3072 waves do not queue on one atomic before their first F evaluation
+                    job = total_jobs;
+                }
                 if (p != tag) {
                     flush_acc(P, acc, tag, lane, w_all, &S.tasks);
                     tag = p;

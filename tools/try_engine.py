@@ -75,6 +75,17 @@ def main():
         out["diag"]["t_exit_us"] = [float(t.min()), float(np.median(t)), float(t.max())]
         tl = (col["t_last_round"] - col["t_start"].min()) / 100.0
         out["diag"]["t_last_us"] = [float(tl.min()), float(np.median(tl)), float(tl.max())]
+        for key in ("t_seeded", "t_first_lead"):
+            if key in col:
+                v = col[key][(col[key] > 0) & (col[key] < 2 ** 62)]
+                if v.size:
+                    tv = (v - col["t_start"].min()) / 100.0
+                    out["diag"][key + "_us"] = [float(tv.min()), float(np.median(tv)), float(tv.max())]
+        ts = (col["t_start"] - col["t_start"].min()) / 100.0
+        out["diag"]["t_start_us"] = [float(ts.min()), float(np.median(ts)), float(ts.max())]
+        for key in ("leads", "chunks_out", "chunks_in", "records_out", "pool_push", "cellar_out", "tasks"):
+            if key in col:
+                out["diag"][key] = float(col[key].sum())
     print(json.dumps(out, indent=1))
     ctx.close()
 
