@@ -496,6 +496,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if constexpr (DIAG) cs = clk();
                 const int p = (int)(job / shares);
                 const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
+                if (p != tag) {
+                    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
+                    tag = p;
+                }
+                // the bounds load goes out before the claim: waiting for it then leaves the claim (one
+                // contended atomic, not needed before the next job) in flight
+                const double2 ab = P.bounds[p];   // once per job (HBM / L2)
                 if (total_jobs > W) {
                     if (lane == 0) claim = W + g_add(&qctl->jobs.v, 1u);   // next job: latency hides behind this one
                     job_pending = true;
@@ -504,11 +511,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     // 3072 waves do not queue on one atomic before their first F evaluation
                     job = total_jobs;
                 }
-                if (p != tag) {
-                    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
-                    tag = p;
-                }
-                const double2 ab = P.bounds[p];   // once per job (HBM / L2)
                 const double A = ab.x, B = ab.y;
                 double* fm = s_a + base;          // [nnodes + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
                 double* leafa = s_b + base;       // [nnodes]: larea + rarea of node (d,k)
