@@ -57,16 +57,14 @@ __device__ __forceinline__ void dfs_flush(const StreamParams& P, int tag, double
     wave_sum_dd(hi, lo);
     const unsigned mx = wave_max_u(m);
     if (lane == 0 && tasks) {
-        WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
-        atomicAdd(&w->tasks, (unsigned long long)tasks);
-        atomicAdd(&w->leaves, (unsigned long long)leaves);
-        atomicMax(&w->levels, mx);
-        double* q = &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all].x;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
-        double h0 = ld_wt(q), l0 = ld_wt(q + 1);
-        dd_add_dd(h0, l0, hi, lo);
-        st_wt(q, h0);
-        st_wt(q + 1, l0);
+        if (P.per_cu) {
+            WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
+            atomicAdd(&w->tasks, (unsigned long long)tasks);
+            atomicAdd(&w->leaves, (unsigned long long)leaves);
+            atomicMax(&w->levels, mx);
+        }
+        slot_flush(P.ctls[P.first_slot + tag], &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all], tasks,
+                   leaves, mx, hi, lo, w_all);
     }
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
@@ -85,8 +83,9 @@ __global__ __launch_bounds__(DPT) void k_dfs(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += DPT) s_dg[i] = 0ull;
     }
-    for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
-        P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].cu = cu_slot();
+    if (P.per_cu)
+        for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
+            P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
@@ -528,7 +527,7 @@ __global__ __launch_bounds__(DPT) void k_dfs(StreamParams P) {
     const unsigned werr = wave_or_u(err);
     if (lane == 0 && werr) {
         for (int p = 0; p < P.nprob; ++p)
-            atomicOr(&P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].error, werr);
+            atomicOr(&P.ctls[P.first_slot + p].sums.error, werr);
     }
     if constexpr (DIAG) {
         if (lane == 0) {

@@ -75,11 +75,21 @@ struct alignas(128) Line {
     unsigned v;
     unsigned pad[31];
 };
+// Per-integral totals (device-scope atomics at every flush) and the list of waves that flushed an
+// area partial into the slot: gathers and resets read only those partials, not all 4096 of them
+// (a list longer than TCAP falls back to the dense pass).
+constexpr unsigned TCAP = 224;
+struct alignas(128) SlotSums {
+    unsigned long long tasks, leaves, spilled;
+    unsigned levels, error, ntouch, pad;
+};
 struct Ctl {
     Line q_tail;               // chunk slots claimed by producers
     Line q_head;               // tickets taken by idle workgroups
     Line q_tokens;             // tokens - G
     Line jobs;                 // job claims
+    SlotSums sums;
+    unsigned touch[TCAP];      // waves with a partial in this slot (repeats possible)
     unsigned long long hist[2 * AQ_MAX_LEVELS];   // [0,L): tasks per level, [L,2L): accepted per level
 };
 
@@ -144,6 +154,7 @@ struct StreamParams {
     double2* stk;                   // k_dfs: per-lane DFS stacks [wave][SDEPTH][64] {x, F(x)}
     unsigned wstride;               // warea entries per slot (>= waves of any engine's grid)
     LaunchHint* hint;
+    int per_cu;                     // also keep per-workgroup partials (per-CU task counts; lone integrals)
     int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
 };
 
@@ -229,6 +240,26 @@ struct Acc {
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
 };
 
+// Add a wave's totals and double-double area to its integral's slot (lane 0). The area partial is
+// the wave's own (no other wave writes it); its first flush also lists the wave in the slot.
+__device__ __forceinline__ void slot_flush(Ctl& c, double2* part, unsigned t, unsigned l, unsigned m, double hi,
+                                           double lo, unsigned w) {
+    atomicAdd(&c.sums.tasks, (unsigned long long)t);
+    atomicAdd(&c.sums.leaves, (unsigned long long)l);
+    atomicMax(&c.sums.levels, m);
+    double* q = &part->x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
+    double h0 = ld_wt(q), l0 = ld_wt(q + 1);
+    const bool first = h0 == 0.0 && l0 == 0.0;
+    dd_add_dd(h0, l0, hi, lo);
+    st_wt(q, h0);
+    st_wt(q + 1, l0);
+    if (first) {   // (a partial that sums back to zero is listed twice: harmless, gathers dedupe)
+        const unsigned i = atomicAdd(&c.sums.ntouch, 1u);
+        if (i < TCAP) c.touch[i] = w;
+    }
+}
+
 // Flush a wave's accumulators for integral `tag`: counts into this workgroup's partial (three
 // uncontended integer atomics), the double-double area into the wave's own partial (a plain
 // read-modify-write: no other wave touches it), and reset them.
@@ -239,16 +270,14 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
         atomicAdd(wg_tasks, (unsigned long long)t);
-        WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
-        atomicAdd(&w->tasks, (unsigned long long)t);
-        atomicAdd(&w->leaves, (unsigned long long)l);
-        atomicMax(&w->levels, m);
-        double* q = &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all].x;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
-        double h0 = ld_wt(q), l0 = ld_wt(q + 1);
-        dd_add_dd(h0, l0, hi, lo);
-        st_wt(q, h0);
-        st_wt(q + 1, l0);
+        if (P.per_cu) {
+            WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
+            atomicAdd(&w->tasks, (unsigned long long)t);
+            atomicAdd(&w->leaves, (unsigned long long)l);
+            atomicMax(&w->levels, m);
+        }
+        slot_flush(P.ctls[P.first_slot + tag], &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all], t, l, m,
+                   hi, lo, w_all);
     }
     a.hi = a.lo = 0.0;
     a.tasks = a.leaves = a.maxd = 0;
@@ -299,8 +328,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
-    for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
-        P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].cu = cu_slot();
+    if (P.per_cu)
+        for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
+            P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
@@ -970,9 +1000,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (lane == 0) {
         if (werr) {
             for (int p = 0; p < P.nprob; ++p)
-                atomicOr(&P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].error, werr);
+                atomicOr(&P.ctls[P.first_slot + p].sums.error, werr);
         }
-        if (spilled) atomicAdd(&P.parts[(size_t)P.first_slot * gridDim.x + bid].spilled, spilled);
+        if (spilled) atomicAdd(&P.ctls[P.first_slot].sums.spilled, spilled);
         if constexpr (DIAG) {
             atomicAdd(&s_dg[DG_LOCK_SPINS], lock_spins);
             atomicAdd(&s_dg[DG_SPILL_RECORDS], spilled);
@@ -1000,11 +1030,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if (tid == 0) {
             s_dg[DG_T_EXIT] = rtc();
             s_dg[DG_CU] = cu_slot();
-            unsigned long long tasks = 0;
-            for (int p = 0; p < P.nprob; ++p)
-                tasks += __hip_atomic_load(&P.parts[(size_t)(P.first_slot + p) * gridDim.x + blockIdx.x].tasks,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_dg[DG_TASKS] = tasks;
+            s_dg[DG_TASKS] = S.tasks;
             unsigned long long* o = P.diag + (size_t)blockIdx.x * DIAG_WORDS;
             for (int i = 0; i < DIAG_WORDS; ++i) o[i] = s_dg[i];
         }

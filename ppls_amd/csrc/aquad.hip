@@ -280,47 +280,80 @@ __global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* o
     if (threadIdx.x == 0) out[0] = Rec{a, b, integrand<FID>(a, tab), integrand<FID>(b, tab)};
 }
 
+// The area partials of one slot (block of 256 threads): every thread returns the double-double sum
+// of its share, in a fixed order -- thread k takes the listed waves 32k..32k+31 in ascending order
+// (a 4096-bit LDS bitmap dedupes the list), or, past TCAP listed waves, the dense stride.
+__device__ __forceinline__ void slot_area_share(const Ctl& c, const double2* __restrict__ wa, int wstride,
+                                                unsigned* s_bits, double& hi, double& lo) {
+    const unsigned n = c.sums.ntouch;
+    hi = lo = 0.0;
+    if (n <= TCAP && wstride <= 4096) {
+        for (int i = threadIdx.x; i < wstride / 32; i += blockDim.x) s_bits[i] = 0u;
+        __syncthreads();
+        if (threadIdx.x < n) {
+            const unsigned w = c.touch[threadIdx.x];
+            atomicOr(&s_bits[w >> 5], 1u << (w & 31u));
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < wstride / 32; k += blockDim.x) {
+            unsigned m = s_bits[k];
+            while (m) {
+                const int b = __builtin_ctz(m);
+                m &= m - 1u;
+                const double2 v = wa[32 * k + b];
+                dd_add_dd(hi, lo, v.x, v.y);
+            }
+        }
+    } else {
+        for (int i = threadIdx.x; i < wstride; i += blockDim.x) dd_add_dd(hi, lo, wa[i].x, wa[i].y);
+    }
+}
+
 // Gather n slots' totals into a caller device buffer as f64 [area, tasks, accepted, error] rows,
-// ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot sums the
-// slot's per-workgroup partials in a fixed order.
-__global__ __launch_bounds__(256) void k_gather(const WgPart* __restrict__ parts, const double2* __restrict__ warea,
-                                                int G, int wstride, int first, int n, int nslots,
-                                                double* __restrict__ out) {
+// ready for one collective (counts are exact in f64 below 2^53). One workgroup per slot: counts
+// from the slot's sums, the area from the listed wave partials in a fixed order.
+__global__ __launch_bounds__(256) void k_gather(const Ctl* __restrict__ ctls, const double2* __restrict__ warea,
+                                                int wstride, int first, int n, int nslots, double* __restrict__ out) {
     __shared__ double s_h[4], s_lo[4];
-    __shared__ unsigned long long s_t[4], s_l[4];
-    __shared__ unsigned s_e[4];
+    __shared__ unsigned s_bits[128];
     const int slot = (first + (int)blockIdx.x) % nslots;
-    const WgPart* w = parts + (size_t)slot * G;
-    const double2* wa = warea + (size_t)slot * wstride;
-    double hi = 0.0, lo = 0.0;
-    unsigned long long t = 0, l = 0;
-    unsigned e = 0;
-    for (int i = threadIdx.x; i < G; i += blockDim.x) {
-        t += w[i].tasks;
-        l += w[i].leaves;
-        e |= w[i].error;
-    }
-    for (int i = threadIdx.x; i < wstride; i += blockDim.x) dd_add_dd(hi, lo, wa[i].x, wa[i].y);
+    const Ctl& c = ctls[slot];
+    double hi, lo;
+    slot_area_share(c, warea + (size_t)slot * wstride, wstride, s_bits, hi, lo);
     wave_sum_dd(hi, lo);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        t += __shfl_xor(t, o, 64);
-        l += __shfl_xor(l, o, 64);
-        e |= (unsigned)__shfl_xor((int)e, o, 64);
-    }
     const unsigned wv = threadIdx.x >> 6;
-    if (lane_id() == 0) { s_h[wv] = hi; s_lo[wv] = lo; s_t[wv] = t; s_l[wv] = l; s_e[wv] = e; }
+    if (lane_id() == 0) { s_h[wv] = hi; s_lo[wv] = lo; }
     __syncthreads();
     if (threadIdx.x == 0) {
         double H = 0.0, Lo = 0.0;
-        unsigned long long T = 0, L = 0;
-        unsigned E = 0;
-        for (int k = 0; k < 4; ++k) { dd_add_dd(H, Lo, s_h[k], s_lo[k]); T += s_t[k]; L += s_l[k]; E |= s_e[k]; }
+        for (int k = 0; k < 4; ++k) dd_add_dd(H, Lo, s_h[k], s_lo[k]);
         double* o = out + 4 * blockIdx.x;
         o[0] = H + Lo;
-        o[1] = (double)T;
-        o[2] = (double)L;
-        o[3] = (double)E;
+        o[1] = (double)c.sums.tasks;
+        o[2] = (double)c.sums.leaves;
+        o[3] = (double)c.sums.error;
+    }
+}
+
+// Return slots [first, first + n) to the all-zero state a launch needs: the listed (or, past TCAP,
+// all) area partials, the sums and the queue words; the histograms when they were written.
+__global__ __launch_bounds__(256) void k_reset(Ctl* __restrict__ ctls, double2* __restrict__ warea, int wstride,
+                                               int first, int zero_hist) {
+    const int slot = first + (int)blockIdx.x;
+    Ctl& c = ctls[slot];
+    double2* wa = warea + (size_t)slot * wstride;
+    const unsigned n = c.sums.ntouch;
+    if (n <= TCAP) {
+        if (threadIdx.x < n) wa[c.touch[threadIdx.x]] = make_double2(0.0, 0.0);
+    } else {
+        for (int i = threadIdx.x; i < wstride; i += blockDim.x) wa[i] = make_double2(0.0, 0.0);
+    }
+    if (zero_hist)
+        for (int i = threadIdx.x; i < 2 * AQ_MAX_LEVELS; i += blockDim.x) c.hist[i] = 0ull;
+    __syncthreads();   // every thread has read ntouch / touch before they are cleared
+    if (threadIdx.x == 0) {
+        c.sums = SlotSums{};
+        c.q_tail.v = 0u; c.q_head.v = 0u; c.q_tokens.v = 0u; c.jobs.v = 0u;
     }
 }
 
@@ -395,7 +428,8 @@ struct aq_ctx {
     WgPart* d_parts = nullptr;         // NSLOTS x grid per-workgroup partials
     double2* d_warea = nullptr;        // NSLOTS x grid*NW per-wave double-double areas
     double2* h_warea = nullptr;        // pinned, grid*NW entries
-    bool dirty[NSLOTS] = {};           // slot's ctl / parts used since they were last zeroed
+    bool dirty[NSLOTS] = {};           // slot's sums / area partials used since they were last reset
+    bool parts_dirty[NSLOTS] = {};     // slot's per-workgroup partials written (per-CU launches)
     bool slot_hist[NSLOTS] = {};
     double2* d_bounds = nullptr;       // NSLOTS {a, b}
     double2* h_bounds = nullptr;       // pinned staging ring, NSTAGE x NSLOTS (a launch's copy may still be
@@ -429,6 +463,7 @@ struct aq_ctx {
     size_t eval_cap = 0;
     // host staging
     WgPart* h_parts = nullptr;         // pinned, grid entries
+    SlotSums* h_sums = nullptr;        // pinned, one
     unsigned long long* h_hist = nullptr;  // pinned, 2 * AQ_MAX_LEVELS
     DevResults* h_lres = nullptr;      // pinned
     HostOut last;
@@ -445,20 +480,29 @@ struct aq_ctx {
 
 namespace {
 
-// Zero the control blocks and partials of slots [s, s+k) if any was used since it was last zeroed;
-// the zeroed range is extended to a batch of 64 slots, so sequential use costs one memset pair per
-// 64 integrals and a launch needs no memset of its own.
+// Return slots [s, s+k) to the all-zero state if any was used since it was last reset: k_reset
+// clears only what the slots' lists name (sums, queue words, listed area partials), so a reset
+// costs bytes per touched wave, not 64 KiB per slot; per-workgroup partials (per-CU launches only)
+// are cleared with a memset of just those slots.
 int ensure_clean(aq_ctx* c, int s, int k) {
-    bool need = false;
-    for (int i = s; i < s + k; ++i) need |= c->dirty[i];
-    if (!need) return AQ_OK;
-    const int e = std::min(NSLOTS, std::max(s + k, s + 64));
-    for (int i = s; i < e; ++i) c->dirty[i] = false;
-    AQ_HIP(hipMemsetAsync(c->d_ctl + s, 0, sizeof(Ctl) * (size_t)(e - s), c->stream));
-    AQ_HIP(hipMemsetAsync(c->d_parts + (size_t)s * c->grid, 0, sizeof(WgPart) * (size_t)(e - s) * c->grid,
-                          c->stream));
-    AQ_HIP(hipMemsetAsync(c->d_warea + (size_t)s * c->wstride, 0, sizeof(double2) * (size_t)(e - s) * c->wstride,
-                          c->stream));
+    bool need = false, hist = false;
+    for (int i = s; i < s + k; ++i) {
+        need |= c->dirty[i];
+        hist |= c->dirty[i] && c->slot_hist[i];
+    }
+    if (need) {
+        hipLaunchKernelGGL(k_reset, dim3(k), dim3(256), 0, c->stream, c->d_ctl, c->d_warea, c->wstride, s, hist ? 1 : 0);
+        AQ_HIP(hipGetLastError());
+        for (int i = s; i < s + k; ++i) c->dirty[i] = false;
+    }
+    for (int i = s; i < s + k;) {
+        if (!c->parts_dirty[i]) { ++i; continue; }
+        int j = i;
+        while (j < s + k && c->parts_dirty[j]) c->parts_dirty[j++] = false;
+        AQ_HIP(hipMemsetAsync(c->d_parts + (size_t)i * c->grid, 0, sizeof(WgPart) * (size_t)(j - i) * c->grid,
+                              c->stream));
+        i = j;
+    }
     return AQ_OK;
 }
 
@@ -521,6 +565,7 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.stk = ctx->d_stk;
     P.wstride = (unsigned)ctx->wstride;
     P.hint = ctx->d_hint;
+    P.per_cu = k < 16 ? 1 : 0;   // per-CU task counts for lone integrals (the reference's per-worker printout)
     // multi-integral stream launches size their jobs from the previous launch's tasks per integral,
     // when that launch integrated the same integrand at the same tolerance (a context that switches
     // workload starts from the default shares and a fresh hint). Not for shards: every shard of an
@@ -564,6 +609,7 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     }
     for (int i = first_slot; i < first_slot + k; ++i) {
         ctx->dirty[i] = true;
+        ctx->parts_dirty[i] = ctx->parts_dirty[i] || P.per_cu;
         ctx->slot_hist[i] = HIST;
     }
     return AQ_OK;
@@ -582,8 +628,10 @@ void fill_result(const HostOut& h, aq_result* out) {
 }
 
 int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
-    AQ_HIP(hipMemcpyAsync(ctx->h_parts, ctx->d_parts + (size_t)slot * ctx->grid, sizeof(WgPart) * (size_t)ctx->grid,
-                          hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->parts_dirty[slot])
+        AQ_HIP(hipMemcpyAsync(ctx->h_parts, ctx->d_parts + (size_t)slot * ctx->grid,
+                              sizeof(WgPart) * (size_t)ctx->grid, hipMemcpyDeviceToHost, ctx->stream));
+    AQ_HIP(hipMemcpyAsync(ctx->h_sums, &ctx->d_ctl[slot].sums, sizeof(SlotSums), hipMemcpyDeviceToHost, ctx->stream));
     const size_t nw = (size_t)ctx->wstride;
     AQ_HIP(hipMemcpyAsync(ctx->h_warea, ctx->d_warea + (size_t)slot * nw, sizeof(double2) * nw, hipMemcpyDeviceToHost,
                           ctx->stream));
@@ -596,14 +644,17 @@ int fetch_slot(aq_ctx* ctx, int slot, aq_result* out) {
     double hi = 0.0, lo = 0.0;
     for (size_t i = 0; i < nw; ++i) dd_add_dd(hi, lo, ctx->h_warea[i].x, ctx->h_warea[i].y);
     h.area = hi + lo;
-    for (int i = 0; i < ctx->grid; ++i) {
-        const WgPart& w = ctx->h_parts[i];
-        h.tasks += w.tasks;
-        h.leaves += w.leaves;
-        h.spilled += w.spilled;
-        h.levels = std::max(h.levels, w.levels);
-        h.error |= w.error;
-        if (w.tasks) h.cu[w.cu % AQ_CU_SLOTS] += w.tasks;
+    const SlotSums& sm = *ctx->h_sums;
+    h.tasks = sm.tasks;
+    h.leaves = sm.leaves;
+    h.spilled = sm.spilled;
+    h.levels = sm.levels;
+    h.error = sm.error;
+    if (ctx->parts_dirty[slot]) {   // per-CU counts: lone-integral launches keep per-workgroup partials
+        for (int i = 0; i < ctx->grid; ++i) {
+            const WgPart& w = ctx->h_parts[i];
+            if (w.tasks) h.cu[w.cu % AQ_CU_SLOTS] += w.tasks;
+        }
     }
     if (ctx->slot_hist[slot]) memcpy(h.hist, ctx->h_hist, sizeof(h.hist));
     ctx->last_valid = true;
@@ -698,6 +749,7 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipMalloc(&c->d_ready, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
     AQ_HIP(hipMemset(c->d_ready, 0, sizeof(unsigned) * (size_t)QCAP * READY_STRIDE));
     AQ_HIP(hipHostMalloc(&c->h_parts, sizeof(WgPart) * (size_t)c->grid, hipHostMallocDefault));
+    AQ_HIP(hipHostMalloc(&c->h_sums, sizeof(SlotSums), hipHostMallocDefault));
     AQ_HIP(hipHostMalloc(&c->h_hist, sizeof(unsigned long long) * 2 * AQ_MAX_LEVELS, hipHostMallocDefault));
     AQ_HIP(hipHostMalloc(&c->h_lres, sizeof(DevResults), hipHostMallocDefault));
     AQ_HIP(hipMalloc(&c->d_lres, sizeof(DevResults)));
@@ -737,6 +789,7 @@ void aq_ctx_destroy(aq_ctx* c) {
     for (int i = 0; i < NSTAGE; ++i)
         if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
     if (c->h_parts) (void)hipHostFree(c->h_parts);
+    if (c->h_sums) (void)hipHostFree(c->h_sums);
     if (c->h_warea) (void)hipHostFree(c->h_warea);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->h_lres) (void)hipHostFree(c->h_lres);
@@ -810,8 +863,8 @@ int aq_gather_results(aq_ctx* ctx, int first_slot, int n, void* d_out) {
     if (!ctx || !d_out || n < 0 || n > NSLOTS || first_slot < 0 || first_slot >= NSLOTS) return AQ_EINVAL;
     if (n == 0) return AQ_OK;
     AQ_HIP(hipSetDevice(ctx->device));
-    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_parts, ctx->d_warea, ctx->grid,
-                       ctx->wstride, first_slot, n, NSLOTS, (double*)d_out);
+    hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, ctx->stream, ctx->d_ctl, ctx->d_warea, ctx->wstride,
+                       first_slot, n, NSLOTS, (double*)d_out);
     AQ_HIP(hipGetLastError());
     return AQ_OK;
 }
