@@ -64,24 +64,37 @@ __device__ __forceinline__ Step task_step(double l, double r, double fl, double 
     return s;
 }
 
-// K trapezoid steps at once (K records per lane); every lane of the wave calls it (inactive lanes
-// pass a harmless record, e.g. l = r = 1, F = 0).
+// K trapezoid steps at once (K records per lane), with every area DOUBLED: the products
+// (fl+fr)*(r-l) etc. of :185/:189/:190 without their '/2'. Halving is exact and commutes with
+// rounding as long as nothing falls below 2^-1021 (no doubled area or difference of the built
+// integrands comes near: |F| >= 1 for cosh^4, and the smallest nonzero |F(l)+F(r)| * width of
+// sin(1/x) at the depth cap is > 2^-200), so
+//   larea + rarea        == (L2 + R2) / 2           (x/2 + y/2 rounds like (x + y)/2)
+//   (larea+rarea)-lrarea == ((L2 + R2) - LR2) / 2
+//   |d / 2| > eps        <=> |d| > 2*eps            (2*eps exact)
+// -- every decision of :191 is bit-identical and each accepted area is exactly half of `area2`;
+// the caller halves its accumulator once (flush). Saves the three '/2' multiplies per task.
+// Every lane of the wave calls it (inactive lanes pass a harmless record, e.g. l = r = 1, F = 0).
+struct Step2 {
+    double fmid, area2;   // F(mid) and 2 * (larea + rarea)
+    bool refine;
+};
 template <int FID, int K>
 __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (&r)[K], const double (&fl)[K],
-                                            const double (&fr)[K], double eps, const ExpEntry* __restrict__ tab,
-                                            Step (&s)[K], const ExpConsts& kk = ExpConsts{}, int range_hint = -1) {
+                                            const double (&fr)[K], double eps2, const ExpEntry* __restrict__ tab,
+                                            Step2 (&s)[K], const ExpConsts& kk = ExpConsts{}, int range_hint = -1) {
     double mid[K], fmid[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) mid[k] = (l[k] + r[k]) / 2;   // :187
     integrand_k<FID, K>(mid, fmid, tab, kk, range_hint);       // :188
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const double lrarea = (fl[k] + fr[k]) * (r[k] - l[k]) / 2;   // :185
-        s[k].mid = mid[k];
+        const double lr2 = (fl[k] + fr[k]) * (r[k] - l[k]);           // 2 * lrarea, :185
+        const double l2 = (fl[k] + fmid[k]) * (mid[k] - l[k]);        // 2 * larea,  :189
+        const double r2 = (fmid[k] + fr[k]) * (r[k] - mid[k]);        // 2 * rarea,  :190
         s[k].fmid = fmid[k];
-        s[k].larea = (fl[k] + fmid[k]) * (mid[k] - l[k]) / 2;         // :189
-        s[k].rarea = (fmid[k] + fr[k]) * (r[k] - mid[k]) / 2;         // :190
-        s[k].refine = fabs((s[k].larea + s[k].rarea) - lrarea) > eps;  // :191
+        s[k].area2 = l2 + r2;
+        s[k].refine = fabs(s[k].area2 - lr2) > eps2;                  // :191 (strict >)
     }
 }
 

@@ -265,7 +265,7 @@ __device__ __forceinline__ void slot_flush(Ctl& c, double2* part, unsigned t, un
 // read-modify-write: no other wave touches it), and reset them.
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all,
                                           unsigned long long* wg_tasks) {
-    double hi = a.hi, lo = a.lo;
+    double hi = 0.5 * a.hi, lo = 0.5 * a.lo;   // the wave accumulates doubled areas (exact halving)
     wave_sum_dd(hi, lo);
     const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
@@ -334,6 +334,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
+    const double eps2 = 2.0 * eps;   // the rounds compare doubled areas (task_step_k)
     const int max_depth = P.max_depth;
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
     unsigned shares = (unsigned)P.shares;
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         acc.maxd = max(acc.maxd, d + 1u);
                         if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
                         if (d == dstar) {
-                            dd_add(acc.hi, acc.lo, leafarea);                 // :199 -> :149
+                            dd_add(acc.hi, acc.lo, 2.0 * leafarea);           // :199 -> :149 (doubled, exact)
                             ++acc.leaves;
                             if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
                         } else if ((int)d + 1 >= max_depth) {
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                                 acc.maxd = max(acc.maxd, d + 1u);
                                 if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
                                 if (d == dstar) {
-                                    dd_add(acc.hi, acc.lo, leafa[d * nb + kk]);   // :199 -> :149
+                                    dd_add(acc.hi, acc.lo, 2.0 * leafa[d * nb + kk]);   // :199 -> :149 (doubled)
                                     ++acc.leaves;
                                     if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
                                 } else if ((int)d + 1 >= max_depth) {
@@ -930,9 +931,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned d = dt & 255u;
         const int rtag = (int)(dt >> 8);
         const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
-        Step st[2];
+        Step2 st[2];
         // both midpoints lie in [pa, pb]: one range test for the pair
-        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps, tab, st, kk, FID == F_COSH4 ? (int)cosh_main_span(pa, pb) : -1);
+        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps2, tab, st, kk, FID == F_COSH4 ? (int)cosh_main_span(pa, pb) : -1);
         // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
         // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
         // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
@@ -951,8 +952,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         acc.ul += (unsigned)__popcll(l0m) + (unsigned)__popcll(l1m);
         acc.maxd = max(acc.maxd, act ? d + 1u : 0u);
         // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-        masked_add(acc.hi, st[0].larea + st[0].rarea, l0m);
-        masked_add(acc.hi, st[1].larea + st[1].rarea, l1m);
+        masked_add(acc.hi, st[0].area2, l0m);   // doubled areas: halved at flush
+        masked_add(acc.hi, st[1].area2, l1m);
         mixed |= (__ballot(rtag != tag) & am) != 0ull;     // the invariant, checked (error if broken)
         if (HIST) {
             if (act) {
