@@ -89,16 +89,22 @@ __device__ __forceinline__ double expm1_glibc_small(double x) {
 // v_div_fmas / v_div_fixup, which are identities in this range (no operand needs rescaling, no
 // special value). They are dropped because v_div_scale / v_div_fmas pass a flag through VCC, and
 // that single register serialises any two divisions a wave would otherwise overlap.
-__device__ __forceinline__ double half_recip(double t) {
+#ifndef AQ_RCP_NEWTON
+#define AQ_RCP_NEWTON 2
+#endif
+template <int NEWTON = AQ_RCP_NEWTON>
+__device__ __forceinline__ double half_recip_n(double t) {
     double y = __builtin_amdgcn_rcp(t);
-    double e = __fma_rn(-t, y, 1.0);
-    y = __fma_rn(y, e, y);
-    e = __fma_rn(-t, y, 1.0);
-    y = __fma_rn(y, e, y);
+#pragma unroll
+    for (int i = 0; i < NEWTON; ++i) {
+        const double e = __fma_rn(-t, y, 1.0);
+        y = __fma_rn(y, e, y);
+    }
     const double q = 0.5 * y;
     const double r = __fma_rn(-t, q, 0.5);
     return __fma_rn(r, y, q);
 }
+__device__ __forceinline__ double half_recip(double t) { return half_recip_n<>(t); }
 
 // glibc __ieee754_cosh.
 __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restrict__ tab) {
@@ -203,7 +209,7 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #pragma unroll
     for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < AQ_RCP_NEWTON; ++it) {
 #pragma unroll
         for (int k = 0; k < K; ++k) y[k] = __fma_rn(y[k], __fma_rn(-t[k], y[k], 1.0), y[k]);
     }

@@ -56,7 +56,8 @@ constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM
 constexpr int GIVE_ROUNDS = 4;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
-constexpr int MAXK = 16384;         // max integrals per launch (tag: 24 bits of the pair's dt word)
+constexpr int PCU_MAXK = 16;        // launches of fewer integrals keep per-workgroup (per-CU) counts
+constexpr int MAXK = 65536;         // max integrals per launch (tag: 24 bits of the pair's dt word)
 constexpr int DEFAULT_GSPLIT = 32;  // a multi-integral launch's job = the share of this many waves
 constexpr unsigned TASKS_PER_JOB = 15000;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
@@ -176,7 +177,7 @@ struct WgState {
     int idle;            // waves with nothing left (no pairs, pool empty, nothing to seed)
     int phase;           // 0 running, 1 a leader wave is at the HBM queue, 2 exit
     int busy_token;      // the workgroup holds one token of the HBM-queue protocol
-    unsigned exited;     // waves past the loop (adaptive launches)
+    unsigned exited;     // waves past the loop (adaptive and per-CU launches)
     unsigned long long tasks;   // tasks this workgroup ran (adaptive launches)
 };
 
@@ -242,11 +243,7 @@ struct Acc {
 
 // Add a wave's totals and double-double area to its integral's slot (lane 0). The area partial is
 // the wave's own (no other wave writes it); its first flush also lists the wave in the slot.
-__device__ __forceinline__ void slot_flush(Ctl& c, double2* part, unsigned t, unsigned l, unsigned m, double hi,
-                                           double lo, unsigned w) {
-    atomicAdd(&c.sums.tasks, (unsigned long long)t);
-    atomicAdd(&c.sums.leaves, (unsigned long long)l);
-    atomicMax(&c.sums.levels, m);
+__device__ __forceinline__ bool area_flush(double2* part, double hi, double lo) {
     double* q = &part->x;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
     double h0 = ld_wt(q), l0 = ld_wt(q + 1);
@@ -254,30 +251,41 @@ __device__ __forceinline__ void slot_flush(Ctl& c, double2* part, unsigned t, un
     dd_add_dd(h0, l0, hi, lo);
     st_wt(q, h0);
     st_wt(q + 1, l0);
-    if (first) {   // (a partial that sums back to zero is listed twice: harmless, gathers dedupe)
+    return first;
+}
+__device__ __forceinline__ void slot_flush(Ctl& c, double2* part, unsigned t, unsigned l, unsigned m, double hi,
+                                           double lo, unsigned w) {
+    atomicAdd(&c.sums.tasks, (unsigned long long)t);
+    atomicAdd(&c.sums.leaves, (unsigned long long)l);
+    atomicMax(&c.sums.levels, m);
+    if (area_flush(part, hi, lo)) {   // (a partial that sums back to zero is listed twice: harmless, gathers dedupe)
         const unsigned i = atomicAdd(&c.sums.ntouch, 1u);
         if (i < TCAP) c.touch[i] = w;
     }
 }
 
-// Flush a wave's accumulators for integral `tag`: counts into this workgroup's partial (three
-// uncontended integer atomics), the double-double area into the wave's own partial (a plain
-// read-modify-write: no other wave touches it), and reset them.
+// Flush a wave's accumulators for integral `tag` and reset them: the double-double area into the
+// wave's own partial (a plain read-modify-write: no other wave touches it); the counts into the slot
+// sums (device atomics, spread over the launch's integrals), or -- per-CU launches, where every wave
+// works on the same one or few integrals -- into the workgroup's LDS counts (fold_wg_counts at exit).
+// pc: the per-CU instance's LDS counts, [0,16) tasks, [16,32) accepted, [32,48) levels per integral.
+template <bool PCU>
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all,
-                                          unsigned long long* wg_tasks) {
+                                          WgState& S, unsigned long long* pc) {
     double hi = 0.5 * a.hi, lo = 0.5 * a.lo;   // the wave accumulates doubled areas (exact halving)
     wave_sum_dd(hi, lo);
     const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
-        atomicAdd(wg_tasks, (unsigned long long)t);
-        if (P.per_cu) {
-            WgPart* w = P.parts + (size_t)(P.first_slot + tag) * gridDim.x + blockIdx.x;
-            atomicAdd(&w->tasks, (unsigned long long)t);
-            atomicAdd(&w->leaves, (unsigned long long)l);
-            atomicMax(&w->levels, m);
+        atomicAdd(&S.tasks, (unsigned long long)t);
+        double2* part = &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all];
+        if constexpr (PCU) {
+            atomicAdd(&pc[tag], (unsigned long long)t);
+            atomicAdd(&pc[PCU_MAXK + tag], (unsigned long long)l);
+            atomicMax(&pc[2 * PCU_MAXK + tag], (unsigned long long)m);
+            area_flush(part, hi, lo);   // the slot is marked for dense gathers at exit, not listed
+        } else {
+            slot_flush(P.ctls[P.first_slot + tag], part, t, l, m, hi, lo, w_all);
         }
-        slot_flush(P.ctls[P.first_slot + tag], &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all], t, l, m,
-                   hi, lo, w_all);
     }
     a.hi = a.lo = 0.0;
     a.tasks = a.leaves = a.maxd = 0;
@@ -294,7 +302,10 @@ __device__ __forceinline__ unsigned ring_wrap(unsigned v) {
     else return min(v, v - (unsigned)WCAP);
 }
 
-template <int FID, bool HIST, bool DIAG>
+// PCU: the per-CU instance (launches of < PCU_MAXK integrals, P.per_cu): workgroup counts per
+// integral in LDS, folded into the slot sums once at exit -- a lone integral's 3072 waves would
+// otherwise queue on one slot's atomics at every flush.
+template <int FID, bool HIST, bool DIAG, bool PCU>
 __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // one SoA block (a | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
     // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
@@ -309,6 +320,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     double* const s_fb = s_pr + 4 * LREC;
     __shared__ ExpEntry tab[128];
     __shared__ WgState S;
+    __shared__ unsigned long long s_pc[PCU ? 3 * PCU_MAXK : 1];
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
 
     const unsigned tid = threadIdx.x;
@@ -325,10 +337,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1;
         S.exited = 0; S.tasks = 0;
     }
+    if (PCU && tid < 3u * PCU_MAXK) s_pc[tid] = 0ull;
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
-    if (P.per_cu)
+    if (PCU)
         for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
             P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
@@ -512,7 +525,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             if (k) {
                 if (ptag != tag) {     // the ring's new integral
-                    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
+                    flush_acc<PCU>(P, acc, tag, lane, w_all, S, s_pc);
                     tag = ptag;
                 }
                 bot = 0;
@@ -528,7 +541,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const int p = (int)(job / shares);
                 const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
                 if (p != tag) {
-                    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
+                    flush_acc<PCU>(P, acc, tag, lane, w_all, S, s_pc);
                     tag = p;
                 }
                 // the bounds load goes out before the claim: waiting for it then leaves the claim (one
@@ -995,7 +1008,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     }
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
-    flush_acc(P, acc, tag, lane, w_all, &S.tasks);
+    flush_acc<PCU>(P, acc, tag, lane, w_all, S, s_pc);
     if (mixed) err |= ERRB_OVERFLOW;
     const unsigned werr = wave_or_u(err);
     if (lane == 0) {
@@ -1011,7 +1024,28 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
         // job-size hint for the next adaptive launch: the last wave of each workgroup adds the
         // workgroup's tasks, the last workgroup sets shares per integral for ~TASKS_PER_JOB per job
-        if ((P.adaptive & 2) && atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u) {
+        const bool last = (PCU || (P.adaptive & 2)) && atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u;
+        if (PCU && last) {
+            // per-CU launch: this workgroup's counts per integral, once -- its per-CU row (plain
+            // stores, one writer) and the slot sums (256 workgroups instead of every wave's flushes)
+            for (int p = 0; p < P.nprob; ++p) {
+                const unsigned long long t = __hip_atomic_load(&s_pc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned long long l = __hip_atomic_load(&s_pc[PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned m = (unsigned)__hip_atomic_load(&s_pc[2 * PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                WgPart* w = P.parts + (size_t)(P.first_slot + p) * gridDim.x + bid;
+                w->tasks = t;
+                w->leaves = l;
+                w->levels = m;
+                Ctl& c = P.ctls[P.first_slot + p];
+                if (t) {
+                    atomicAdd(&c.sums.tasks, t);
+                    atomicAdd(&c.sums.leaves, l);
+                    atomicMax(&c.sums.levels, m);
+                }
+                if (bid == 0) atomicMax(&c.sums.ntouch, TCAP + 1u);   // gathers / resets take the dense pass
+            }
+        }
+        if (last && (P.adaptive & 2)) {
             const unsigned long long wt = __hip_atomic_load(&S.tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&P.hint->tasks, wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned g = __hip_atomic_fetch_add(&P.hint->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);

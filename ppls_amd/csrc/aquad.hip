@@ -366,7 +366,7 @@ using namespace aq;
 
 namespace {
 
-constexpr int NSLOTS = 16384;
+constexpr int NSLOTS = 65536;
 constexpr int NSTAGE = 4;          // pinned bounds staging buffers
 constexpr unsigned QCAP = 16384;
 constexpr int DFS_MIN_K = 1 << 30;   // auto engine: k_stream (measured faster); k_dfs on request
@@ -565,7 +565,7 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     P.stk = ctx->d_stk;
     P.wstride = (unsigned)ctx->wstride;
     P.hint = ctx->d_hint;
-    P.per_cu = k < 16 ? 1 : 0;   // per-CU task counts for lone integrals (the reference's per-worker printout)
+    P.per_cu = k < PCU_MAXK ? 1 : 0;   // per-CU task counts for lone integrals (the reference's per-worker printout)
     // multi-integral stream launches size their jobs from the previous launch's tasks per integral,
     // when that launch integrated the same integrand at the same tolerance (a context that switches
     // workload starts from the default shares and a fresh hint). Not for shards: every shard of an
@@ -598,9 +598,15 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
         else
             hipLaunchKernelGGL((k_dfs<FID, HIST, false>), dim3(G), dim3(DPT), 0, ctx->stream, P);
     } else if (P.diag) {
-        hipLaunchKernelGGL((k_stream<FID, HIST, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
+        if (P.per_cu)
+            hipLaunchKernelGGL((k_stream<FID, HIST, true, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
+        else
+            hipLaunchKernelGGL((k_stream<FID, HIST, true, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
     } else {
-        hipLaunchKernelGGL((k_stream<FID, HIST, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
+        if (P.per_cu)
+            hipLaunchKernelGGL((k_stream<FID, HIST, false, true>), dim3(G), dim3(PT), 0, ctx->stream, P);
+        else
+            hipLaunchKernelGGL((k_stream<FID, HIST, false, false>), dim3(G), dim3(PT), 0, ctx->stream, P);
     }
     AQ_HIP(hipGetLastError());
     if (ctx->timing) {
@@ -711,7 +717,7 @@ int aq_ctx_create(int device, aq_ctx** out) {
     AQ_HIP(hipGetDeviceProperties(&prop, device));
     c->num_cus = prop.multiProcessorCount;
     int occ = 0;
-    AQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_stream<F_COSH4, true, false>, PT, 0));
+    AQ_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_stream<F_COSH4, true, false, false>, PT, 0));
     if (occ < 1) {
         delete c;
         return AQ_ENODEV;
