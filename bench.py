@@ -241,8 +241,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (analytic integrand, no dataset)",
-            "config": {"workload": "cosh4 on [0,5], EPSILON=%g (BASELINE configs[1]); one step = a batch of %d "
-                                   "such integrals, each sharded over the GPUs" % (args.eps, B),
+            "config": {"workload": "cosh4 on [0,5], EPSILON=%g (BASELINE %s); one step = a batch of %d "
+                                   "such integrals, each sharded over the GPUs"
+                                   % (args.eps, {1e-10: "configs[1]", 1e-12: "configs[4]"}.get(args.eps, "off-config"), B),
                        "integrand": "cosh(x)^4 (aquadPartA.c:46)", "a": 0.0, "b": 5.0, "eps": args.eps,
                        "tasks_per_integral": int(tot[0, 1]), "accepted_per_integral": int(tot[0, 2]),
                        "parallelism": f"shard{world}" if world > 1 else "single-gpu",

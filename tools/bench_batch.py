@@ -1,5 +1,5 @@
 """a batch of 1 000 000 independent cos h^4 integrals with splitmix64 bounds
-on one MI355X, through the batch front end (aq_integrate_batch: 16384-integral persistent launches,
+on one MI355X, through the batch front end (aq_integrate_batch: 65536-integral persistent launches,
 device gathers, one host sync). Prints accepted subintervals/s and the KAT of §8d (mean leaves of
 the first 10 000 draws: 711.5 at eps=1e-3, 153 330.8 at eps=1e-10).
 
@@ -45,7 +45,7 @@ def main():
     a, b = splitmix64_bounds(args.n)
     out = {"n": args.n}
     for eps in [float(e) for e in args.eps.split(",")]:
-        ctx.integrate_batch(a[:16384], b[:16384], eps)          # warmup
+        ctx.integrate_batch(a[:65536], b[:65536], eps)          # warmup
         best = None
         for _ in range(args.reps):
             t0 = time.perf_counter()
