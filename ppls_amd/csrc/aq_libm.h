@@ -95,10 +95,15 @@ __device__ __forceinline__ double expm1_glibc_small(double x) {
 template <int NEWTON = AQ_RCP_NEWTON>
 __device__ __forceinline__ double half_recip_n(double t) {
     double y = __builtin_amdgcn_rcp(t);
-#pragma unroll
-    for (int i = 0; i < NEWTON; ++i) {
+    if constexpr (NEWTON == 3) {   // second-order step y0 (1 + e + e^2): the error of two Newton steps, one FMA fewer
         const double e = __fma_rn(-t, y, 1.0);
-        y = __fma_rn(y, e, y);
+        y = __fma_rn(y, __fma_rn(e, e, e), y);
+    } else {
+#pragma unroll
+        for (int i = 0; i < NEWTON; ++i) {
+            const double e = __fma_rn(-t, y, 1.0);
+            y = __fma_rn(y, e, y);
+        }
     }
     const double q = 0.5 * y;
     const double r = __fma_rn(-t, q, 0.5);
@@ -209,9 +214,16 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #pragma unroll
     for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
 #pragma unroll
-    for (int it = 0; it < AQ_RCP_NEWTON; ++it) {
+    for (int it = 0; it < (AQ_RCP_NEWTON == 3 ? 0 : AQ_RCP_NEWTON); ++it) {
 #pragma unroll
         for (int k = 0; k < K; ++k) y[k] = __fma_rn(y[k], __fma_rn(-t[k], y[k], 1.0), y[k]);
+    }
+    if (AQ_RCP_NEWTON == 3) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double e = __fma_rn(-t[k], y[k], 1.0);
+            y[k] = __fma_rn(y[k], __fma_rn(e, e, e), y[k]);
+        }
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {

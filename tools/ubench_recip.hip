@@ -2,8 +2,8 @@
 //
 // cosh's main path (aq_libm.h) needs the correctly rounded 0.5 / t for t = exp(|x|) in [1.41, 3.6e9].
 // half_recip_n<N> is v_rcp_f64, N Newton steps on the reciprocal, then the quotient correction
-// q + (0.5 - t*q)*y. This tool counts, over a few billion t, where N = 0 and N = 1 differ from the
-// IEEE division the compiler emits for `0.5 / t` (div_scale / rcp / 2 Newton / div_fmas / div_fixup):
+// q + (0.5 - t*q)*y (N = 3: one second-order step y0 (1 + e + e^2) instead). This tool counts, over
+// a few billion t, where each variant differs from the IEEE division the compiler emits for `0.5 / t` (div_scale / rcp / 2 Newton / div_fmas / div_fixup):
 //   * pass 0: t = exp_glibc(x), x uniform in the main range [0.5*ln2, 22) (the values the kernel sees)
 //   * pass 1: t with random exponent in [0, 31] and random 52-bit mantissa (every bit pattern in range)
 // plus the largest relative error of y after N steps (in units of 2^-53). Per-thread counts are written
@@ -37,7 +37,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 struct Counts {
-    unsigned long long n, bad0, bad1, bad2;
+    unsigned long long n, bad0, bad1, bad2, bad3;
     double relerr_y0, relerr_y1;
 };
 
@@ -46,7 +46,7 @@ __global__ void k_recip(const aq::ExpEntry* __restrict__ gtab, Counts* out, int 
     aq::stage_exp_table(tab, gtab);
     __syncthreads();
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    Counts c = {0, 0, 0, 0, 0.0, 0.0};
+    Counts c = {0, 0, 0, 0, 0, 0.0, 0.0};
     for (int it = 0; it < iters; ++it) {
         const uint64_t z = mix64(seed + (gid * (uint64_t)iters + it) * 0x9E3779B97F4A7C15ull);
         double t;
@@ -63,10 +63,12 @@ __global__ void k_recip(const aq::ExpEntry* __restrict__ gtab, Counts* out, int 
         const double v0 = aq::half_recip_n<0>(t);
         const double v1 = aq::half_recip_n<1>(t);
         const double v2 = aq::half_recip_n<2>(t);
+        const double v3 = aq::half_recip_n<3>(t);
         c.n += 1;
         c.bad0 += (v0 != ref);
         c.bad1 += (v1 != ref);
         c.bad2 += (v2 != ref);
+        c.bad3 += (v3 != ref);
         // relative error of the reciprocal estimate itself, in ulps of 2^-53: |1 - t*y|
         const double y0 = __builtin_amdgcn_rcp(t);
         const double y1 = __fma_rn(y0, __fma_rn(-t, y0, 1.0), y0);
@@ -92,18 +94,19 @@ int main(int argc, char** argv) {
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(h.data(), dout, nt * sizeof(Counts), hipMemcpyDeviceToHost));
-        Counts s = {0, 0, 0, 0, 0.0, 0.0};
+        Counts s = {0, 0, 0, 0, 0, 0.0, 0.0};
         for (const Counts& c : h) {
             s.n += c.n;
             s.bad0 += c.bad0;
             s.bad1 += c.bad1;
             s.bad2 += c.bad2;
+            s.bad3 += c.bad3;
             s.relerr_y0 = std::fmax(s.relerr_y0, c.relerr_y0);
             s.relerr_y1 = std::fmax(s.relerr_y1, c.relerr_y1);
         }
         printf("{\"pass\": %d, \"samples\": %llu, \"mismatch_newton0\": %llu, \"mismatch_newton1\": %llu, "
-               "\"mismatch_newton2\": %llu, \"max_relerr_rcp_ulp53\": %.6g, \"max_relerr_newton1_ulp53\": %.6g}\n",
-               pass, s.n, s.bad0, s.bad1, s.bad2, s.relerr_y0, s.relerr_y1);
+               "\"mismatch_newton2\": %llu, \"mismatch_second_order\": %llu, \"max_relerr_rcp_ulp53\": %.6g, \"max_relerr_newton1_ulp53\": %.6g}\n",
+               pass, s.n, s.bad0, s.bad1, s.bad2, s.bad3, s.relerr_y0, s.relerr_y1);
     }
     CHECK(hipFree(dtab));
     CHECK(hipFree(dout));
