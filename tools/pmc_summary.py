@@ -20,8 +20,27 @@ for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
         names[r["Dispatch_Id"]] = r["Kernel_Name"]
     if not per:
         continue
-    big = sorted(per.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:2]
+    big = sorted(per.items(), key=lambda kv: -max(kv[1].values()))[:2]
     avg = {k: sum(d[1].get(k, 0) for d in big) / len(big) for k in big[0][1]}
-    avg["valu_busy_frac_per_simd_est"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+    if "SQ_ACTIVE_INST_VALU" in avg and avg.get("SQ_WAVE_CYCLES"):
+        avg["valu_busy_frac_per_simd_est"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
     out[eng] = {"kernel": names[big[0][0]][:60], "dispatches": [d[0] for d in big], "avg": avg}
 print(json.dumps(out, indent=1))
+
+# hardware-executed FP64 FLOP of the stream kernel's dispatches (whole-device totals of wave-level
+# instruction counts x 64 lanes; FMA = 2 FLOP, inactive lanes included) -- the PMC cross-check of
+# the algorithmic 38 FLOP per task that bench.py's roofline uses. Pass the kernel's average
+# duration (us, from the kernel-trace run) as argv[2] to get the rate.
+f64 = {}
+for eng, d in out.items():
+    a = d["avg"]
+    if "SQ_INSTS_VALU_FMA_F64" in a:
+        flop = 64.0 * (a.get("SQ_INSTS_VALU_ADD_F64", 0) + a.get("SQ_INSTS_VALU_MUL_F64", 0) +
+                       a.get("SQ_INSTS_VALU_TRANS_F64", 0) + 2.0 * a["SQ_INSTS_VALU_FMA_F64"])
+        f64[eng] = {"fp64_flop_per_dispatch": flop}
+        if len(sys.argv) > 2:
+            t = float(sys.argv[2]) * 1e-6
+            f64[eng]["fp64_tflops_hw"] = flop / t / 1e12
+            f64[eng]["frac_of_78.6"] = flop / t / 78.6e12
+if f64:
+    print(json.dumps({"fp64_hw": f64}, indent=1))

@@ -11,5 +11,5 @@ P2="SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_V
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/tools/try_engine.py" --engine stream --reps 2 --k 2048 > "$OUT/p$i.out" 2>&1 || echo "pass $i failed"
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/tools/try_engine.py" --engine stream --reps 2 --k ${K:-8192} > "$OUT/p$i.out" 2>&1 || echo "pass $i failed"
 done
