@@ -366,6 +366,9 @@ using namespace aq;
 
 namespace {
 
+#ifndef AQ_PCU_SW
+#define AQ_PCU_SW 4   // measured: one integral at eps=1e-12 94 -> 80 us, eps=1e-10 unchanged
+#endif
 constexpr int NSLOTS = 65536;
 constexpr int NSTAGE = 4;          // pinned bounds staging buffers
 constexpr unsigned QCAP = 16384;
@@ -549,7 +552,15 @@ int launch_stream(aq_ctx* ctx, int k, const double* a, const double* b, double e
     if (ctx->gsplit_env > 0) gs = ctx->gsplit_env;
     while (gs > 1 && W % gs != 0) gs >>= 1;
     P.shares = W / gs;
-    P.D = floor_log2((unsigned long long)P.shares * (unsigned long long)nshards) + S_W;
+    // a lone unsharded integral (one share per wave) seeds deeper: more, smaller positions per
+    // share even out the shares' subtrees (only the totals of such a launch are compared)
+    P.D = floor_log2((unsigned long long)P.shares * (unsigned long long)nshards) +
+          ((k < PCU_MAXK && nshards == 1 && !dfs) ? AQ_PCU_SW : S_W);
+    {   // seeding keeps F and flags of every path node of a share in the wave's ring (WCAP slots)
+        const unsigned long long V = (unsigned long long)P.shares * (unsigned long long)nshards;
+        const unsigned long long nb = ((1ull << P.D) + V - 1) / V;
+        if (!dfs && (unsigned long long)(P.D + 1) * nb + 2 > (unsigned long long)WCAP) return AQ_EINVAL;
+    }
     P.epoch = ++ctx->epoch;
     if (P.epoch == 0) P.epoch = ++ctx->epoch;
     P.qcap = QCAP;
