@@ -111,6 +111,9 @@ __device__ __forceinline__ double half_recip_n(double t) {
 }
 __device__ __forceinline__ double half_recip(double t) { return half_recip_n<>(t); }
 
+// glibc's `half*t + half/t` is RN(RN(0.5*t) + h) with h = RN(0.5/t); 0.5*t is exact for the
+// normal t of this range, so RN(0.5*t + h) -- one fma(t, 0.5, h) -- is the same value, bit for bit,
+// one multiply fewer per evaluation.
 // glibc __ieee754_cosh.
 __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restrict__ tab) {
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
@@ -123,7 +126,7 @@ __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restric
             return 1.0 + (t * t) / (w + w);
         }
         const double t = exp_glibc(ax, tab);
-        return 0.5 * t + half_recip(t);     // 0.5 / t, t in [1.41, 3.6e9]
+        return __fma_rn(t, 0.5, half_recip(t));   // 0.5*t + 0.5/t (cosh_tail), t in [1.41, 3.6e9]
     }
     if (ix >= 0x7ff00000u) return x * x;
     if (ix < 0x40862e42u) return 0.5 * exp_glibc(ax, tab);
@@ -228,7 +231,7 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         q[k] = 0.5 * y[k];
-        c[k] = 0.5 * t[k] + __fma_rn(__fma_rn(-t[k], q[k], 0.5), y[k], q[k]);   // 0.5*t + half_recip(t)
+        c[k] = __fma_rn(t[k], 0.5, __fma_rn(__fma_rn(-t[k], q[k], 0.5), y[k], q[k]));   // 0.5*t + half_recip(t)
     }
     return out;
 }

@@ -293,6 +293,35 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
+// Write one pair into LDS slot j of the SoA block (a | b | fa | fm | fb, LREC doubles each). The
+// fields sit 52 x 512 B apart, so with AQ_ASM_PUSH all five go out from ONE address as
+// ds_write2st64 (a, b at 0/52), ds_write (fa at +53248) and ds_write2st64 (fm, fb at 156/208): the
+// compiler pairs only (a, b) and adds the fm / fb offsets (beyond the 16-bit DS offset) per push.
+// Writes only, so nothing waits on them here; LDS operations of one wave complete in order, so the
+// compiler's own later reads of the ring see them, and the "memory" clobber keeps its accesses on
+// their side of the asm.
+#ifndef AQ_ASM_PUSH
+#define AQ_ASM_PUSH 0
+#endif
+__device__ __forceinline__ void push_pair(double* s_pr, unsigned* s_dt, unsigned j, double a, double b, double fa,
+                                          double fm, double fb, unsigned dt) {
+#if AQ_ASM_PUSH
+    static_assert(LREC * 8 == 52 * 512, "push_pair's DS offsets assume 52 x 512 B per field");
+    const unsigned addr = (unsigned)(uintptr_t)(s_pr + j);   // low 32 bits of a flat LDS address = its offset
+    asm volatile(
+        "ds_write2st64_b64 %0, %1, %2 offset1:52\n\t"
+        "ds_write_b64 %0, %3 offset:53248\n\t"
+        "ds_write2st64_b64 %0, %4, %5 offset0:156 offset1:208"
+        :
+        : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb)
+        : "memory");
+#else
+    s_pr[j] = a; s_pr[LREC + j] = b;
+    s_pr[2 * LREC + j] = fa; s_pr[3 * LREC + j] = fm; s_pr[4 * LREC + j] = fb;
+#endif
+    s_dt[j] = dt;
+}
+
 // Ring slot of monotonic ring index i.
 __device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned)WCAP; }
 // Ring slot of b + k for a slot b < WCAP and k < WCAP: one mask (power-of-two ring) or one
@@ -982,13 +1011,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned cdt = dt + 1u;                       // depth + 1, same integral
         if (refine0) {
             const unsigned j = base + ring_wrap(b0s + mbcnt(mask0));
-            s_a[j] = pa; s_b[j] = pm;
-            s_fa[j] = pfa; s_fm[j] = st[0].fmid; s_fb[j] = pfm; s_dt[j] = cdt;
+            push_pair(s_pr, s_dt, j, pa, pm, pfa, st[0].fmid, pfm, cdt);
         }
         if (refine1) {
             const unsigned j = base + ring_wrap(b0s + cnt0 + mbcnt(mask1));
-            s_a[j] = pm; s_b[j] = pb;
-            s_fa[j] = pfm; s_fm[j] = st[1].fmid; s_fb[j] = pfb; s_dt[j] = cdt;
+            push_pair(s_pr, s_dt, j, pm, pb, pfm, st[1].fmid, pfb, cdt);
         }
         top = b0 + cnt0 + (unsigned)__popcll(mask1);
         if constexpr (DIAG) {
