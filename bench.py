@@ -18,7 +18,8 @@ Prints ONE JSON line (rank 0). `value` = accepted subintervals/s over all GPUs; 
 persistent kernel's FP64 rate (38 algorithmic FLOP per task) over its HIP-event
 launch time, against the 78.6 TFLOP/s FP64 vector peak of one MI355X; cpu_baseline is the
 reference binary (oracle/_ref, compiled from /root/reference) run under mpirun on this host's
-cores, or the oracle restatement when that binary cannot run.
+cores, or -- when that binary cannot run -- the bag of tasks on threads (oracle/aq_bag.c), or the
+sequential oracle restatement.
 """
 import argparse
 import json
@@ -62,6 +63,25 @@ def cpu_baseline(eps, target_s=12.0):
                               f"(farmer + {nprocs - 1} workers), {t_total:.1f} s wall incl. MPI startup"}
         except Exception as e:  # fall back to the restatement
             print(f"cpu_baseline: reference binary unusable ({e}); timing the oracle port", file=sys.stderr)
+    # the bag of tasks on threads (oracle/aq_bag.c: farmer + nprocs-1 workers, the reference's algorithm)
+    bag = os.path.join(ROOT, "oracle", "_build", "aq_bag")
+    if os.path.exists(bag) and leaves_golden and eps in (1e-3, 1e-10, 1e-12):
+        try:
+            runs, t_total = 0, 0.0
+            while t_total < target_s and runs < 50:
+                t0 = time.perf_counter()
+                out = subprocess.run([bag, "-n", str(nprocs), "-e", repr(eps)], capture_output=True, text=True,
+                                     timeout=120, check=True).stdout
+                t_total += time.perf_counter() - t0
+                runs += 1
+                if sum(int(v) for v in out.strip().splitlines()[-1].split()) != tasks_golden:
+                    raise RuntimeError("bag-of-tasks task total mismatch")
+            return {"value": leaves_golden * runs / t_total, "unit": "accepted subintervals/s", "cores": nprocs,
+                    "kind": "port",
+                    "sample": f"{runs} full runs of oracle/aq_bag (the reference's farmer/worker on threads, eps={eps}), "
+                              f"farmer + {nprocs - 1} workers, {t_total:.1f} s wall"}
+        except Exception as e:
+            print(f"cpu_baseline: oracle/aq_bag unusable ({e}); timing the sequential oracle", file=sys.stderr)
     from oracle import pyoracle as O
     runs, t_total, leaves = 0, 0.0, 0
     while t_total < target_s and runs < 400:
