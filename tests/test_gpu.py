@@ -351,3 +351,26 @@ def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
                 assert (tot == np.array([g10["tasks"], g10["leaves"]])).all()
     finally:
         ctx.set_level_histograms(True)
+
+
+# Deeper trees than the committed fixtures (counts of the reference's
+# arithmetic): up to 150 M tasks and depth 31 in one launch, alone and as a small batch.
+DEEP = {1e-14: (30870291, 15435146), 1e-15: (66989173, 33494587), 1e-16: (150257851, 75128926)}
+
+
+@pytest.mark.parametrize("eps", sorted(DEEP))
+def test_deep_trees(ctx, oracle, eps):
+    from ppls_amd import Problem
+    ctx.set_level_histograms(False)
+    try:
+        r = ctx.integrate(Problem(eps=eps))
+        assert (r.tasks, r.accepted) == DEEP[eps]
+        assert sum(r.tasks_per_cu.values()) == r.tasks
+        ctx.integrate_many_async(np.zeros(4), np.full(4, 5.0), eps, first_slot=0)
+        got = [ctx.fetch(i) for i in range(4)]
+        assert all((g.tasks, g.accepted) == DEEP[eps] for g in got)
+        if eps == 1e-14:
+            o = oracle.integrate(eps=eps)
+            assert all(abs(g.area - o.area) <= AREA_RTOL * o.area for g in got + [r])
+    finally:
+        ctx.set_level_histograms(True)

@@ -127,3 +127,10 @@ def test_batch_bounds_and_kat(oracle, batch_golden):
     assert (t == 2 * lv - 1).all()
     # SURVEY §8d KAT: first 10 000 draws -> mean leaves 711.5 at eps=1e-3
     assert abs(batch_golden["mean_leaves_eps1e-3"] - 711.5) < 0.05
+
+
+def test_oracle_deep_eps(oracle):
+    # eps=1e-14 -> T=30 870 291, L=15 435 146, measured there by a
+    # verbatim replay of the reference's task arithmetic (it reproduced every MPI total)
+    r = oracle.integrate(eps=1e-14)
+    assert (r.tasks, r.leaves) == (30870291, 15435146)
