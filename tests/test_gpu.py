@@ -374,3 +374,15 @@ def test_deep_trees(ctx, oracle, eps):
             assert all(abs(g.area - o.area) <= AREA_RTOL * o.area for g in got + [r])
     finally:
         ctx.set_level_histograms(True)
+
+
+@pytest.mark.parametrize("eps", [1e-10, 1e-12])
+def test_sin_recip_deeper(ctx, oracle, eps):
+    """Config 4's integrand past the fixture's eps=1e-9 (sin(1/x) counts are robust to
+    +-1 ulp of sin at 1e-9 and 1e-12, so the device libm's faithful sin must reproduce them)."""
+    from ppls_amd import Problem
+    o = oracle.integrate(integrand=1, a=1e-4, b=1.0, eps=eps)
+    r = ctx.integrate(Problem(1, 1e-4, 1.0, eps))
+    assert (r.tasks, r.accepted, r.levels) == (o.tasks, o.leaves, o.levels)
+    assert r.tasks_per_level == o.tasks_per_level
+    assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
