@@ -58,8 +58,14 @@ constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers ne
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr int PCU_MAXK = 16;        // launches of fewer integrals keep per-workgroup (per-CU) counts
 constexpr int MAXK = 65536;         // max integrals per launch (tag: 24 bits of the pair's dt word)
-constexpr int DEFAULT_GSPLIT = 32;  // a multi-integral launch's job = the share of this many waves
-constexpr unsigned TASKS_PER_JOB = 15000;   // adaptive job size: a job holds about this many tasks
+#ifndef AQ_GSPLIT_DEFAULT
+#define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
+#endif
+constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
+#ifndef AQ_TASKS_PER_JOB
+#define AQ_TASKS_PER_JOB 40000   // A/B at 8192 integrals per launch: 8k 35.4, 15k 33.7, 25k 33.6, 40k 33.1, 60k 33.3, 100k 37.0 ms
+#endif
+constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches 64 cellar pairs
