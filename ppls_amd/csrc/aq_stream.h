@@ -50,10 +50,19 @@ constexpr int CH = 256;             // pairs per HBM queue chunk (<= PCAP: a chu
 #define AQ_S_W 2
 #endif
 constexpr int S_W = AQ_S_W;              // seed depth D = floor(log2 V) + S_W: 3 or 4 positions per share
-constexpr int GIVE_MIN = 96;        // a busy wave feeds the pool for idle siblings only above this size
+#ifndef AQ_GIVE_MIN
+#define AQ_GIVE_MIN 96
+#endif
+constexpr int GIVE_MIN = AQ_GIVE_MIN;        // a busy wave feeds the pool for idle siblings only above this size
 constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup donates from its pool
-constexpr int POLL_ROUNDS = 32;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
-constexpr int GIVE_ROUNDS = 4;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
+#ifndef AQ_POLL_ROUNDS
+#define AQ_POLL_ROUNDS 64   // A/B r01q (8192 integrals, eps 1e-10): 16 34.26, 32 33.35, 64 32.95 ms per launch
+#endif
+constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
+#ifndef AQ_GIVE_ROUNDS
+#define AQ_GIVE_ROUNDS 8    // with POLL_ROUNDS 64: 8 32.74, 16 32.63 ms, but 16 costs C3 eps=1e-3 6 % (19.5 -> 20.5 ms)
+#endif
+constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr int PCU_MAXK = 16;        // launches of fewer integrals keep per-workgroup (per-CU) counts
