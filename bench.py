@@ -17,14 +17,11 @@ tree after timing.
 Prints ONE JSON line (rank 0). `value` = accepted subintervals/s over all GPUs; roofline is the
 persistent kernel's FP64 rate (38 algorithmic FLOP per task) over its HIP-event
 launch time, against the 78.6 TFLOP/s FP64 vector peak of one MI355X; cpu_baseline is the
-reference binary (oracle/_ref, compiled from /root/reference) run under mpirun on this host's
-cores, or -- when that binary cannot run -- the bag of tasks on threads (oracle/aq_bag.c), or the
-sequential oracle restatement.
+reference's bag of tasks restated on threads (oracle/aq_bag.c) timed on this host's cores.
 """
 import argparse
 import json
 import os
-import shutil
 import subprocess
 import sys
 import time
@@ -37,33 +34,28 @@ FP64_PEAK = 78.6e12         # MI355X FP64 vector peak (256 CU x 2.4 GHz x 128 FL
 GOLDEN = {1e-10: (1464273, 732137), 1e-12: (6606491, 3303246), 1e-8: (319295, 159648), 1e-3: (6567, 3284)}
 
 
+def host_cores():
+    """CPU cores this process may use on this host, and the share it should load: the affinity set,
+    capped by OMP_NUM_THREADS where the pool sets it (the GPU box: 16 cores per GPU)."""
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = ncpu
+    try:
+        share = min(ncpu, int(os.environ.get("OMP_NUM_THREADS", ncpu)))
+    except ValueError:
+        pass
+    return ncpu, max(2, share)
+
+
 def cpu_baseline(eps, target_s=12.0):
-    """Time the reference on this host's CPU cores (bounded sample), before any GPU init."""
-    tag = {1e-3: "1e-3", 1e-10: "1e-10", 1e-12: "1e-12"}.get(eps, "none")
-    ref = os.path.join(ROOT, "oracle", "_ref", "aquadPartA_eps" + tag)
-    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    nprocs = max(2, min(8, ncpu))  # farmer + up to 7 workers (the survey's P=8 config)
+    """The reference's algorithm timed on this host's CPU cores (bounded sample), before any GPU init.
+
+    SURVEY §8c/§8d: on the GPU host the CPU baseline is the build's own restatement of the farmer /
+    worker bag of tasks (oracle/aq_bag.c: farmer + P-1 workers on threads, the reference's LIFO bag,
+    dispatch loop and task body over the host libm), with P = the cores this process may load. Its
+    totals must equal the reference's. (The reference binary itself is timed in the build container,
+    BASELINE.md; it is not shipped here.) Falls back to the sequential oracle restatement."""
     tasks_golden, leaves_golden = GOLDEN.get(eps, (None, None))
-    if os.path.exists(ref) and os.path.exists(mpirun) and leaves_golden:
-        try:
-            runs, t_total = 0, 0.0
-            while t_total < target_s and runs < 50:
-                t0 = time.perf_counter()
-                out = subprocess.run([mpirun, "-n", str(nprocs), ref], capture_output=True, text=True, timeout=120,
-                                     check=True).stdout
-                t_total += time.perf_counter() - t0
-                runs += 1
-                counts = [int(v) for v in out.strip().splitlines()[-1].split()]
-                if sum(counts) != tasks_golden:
-                    raise RuntimeError("reference task total mismatch")
-            return {"value": leaves_golden * runs / t_total, "unit": "accepted subintervals/s", "cores": nprocs,
-                    "kind": "reference",
-                    "sample": f"{runs} full runs of the reference binary (eps={eps}) under mpirun -n {nprocs} "
-                              f"(farmer + {nprocs - 1} workers), {t_total:.1f} s wall incl. MPI startup"}
-        except Exception as e:  # fall back to the restatement
-            print(f"cpu_baseline: reference binary unusable ({e}); timing the oracle port", file=sys.stderr)
-    # the bag of tasks on threads (oracle/aq_bag.c: farmer + nprocs-1 workers, the reference's algorithm)
+    ncpu, nprocs = host_cores()
     bag = os.path.join(ROOT, "oracle", "_build", "aq_bag")
     if os.path.exists(bag) and leaves_golden and eps in (1e-3, 1e-10, 1e-12):
         try:
@@ -77,9 +69,10 @@ def cpu_baseline(eps, target_s=12.0):
                 if sum(int(v) for v in out.strip().splitlines()[-1].split()) != tasks_golden:
                     raise RuntimeError("bag-of-tasks task total mismatch")
             return {"value": leaves_golden * runs / t_total, "unit": "accepted subintervals/s", "cores": nprocs,
-                    "kind": "port",
-                    "sample": f"{runs} full runs of oracle/aq_bag (the reference's farmer/worker on threads, eps={eps}), "
-                              f"farmer + {nprocs - 1} workers, {t_total:.1f} s wall"}
+                    "host_cpus": ncpu, "kind": "port",
+                    "sample": f"{runs} full integrals (cosh4 [0,5], eps={eps}) by oracle/aq_bag -- the reference's "
+                              f"farmer/worker bag of tasks on threads, farmer + {nprocs - 1} workers on {nprocs} of "
+                              f"this host's {ncpu} CPUs -- {t_total:.1f} s wall"}
         except Exception as e:
             print(f"cpu_baseline: oracle/aq_bag unusable ({e}); timing the sequential oracle", file=sys.stderr)
     from oracle import pyoracle as O
@@ -90,8 +83,9 @@ def cpu_baseline(eps, target_s=12.0):
         t_total += time.perf_counter() - t0
         runs += 1
         leaves += r.leaves
-    return {"value": leaves / t_total, "unit": "accepted subintervals/s", "cores": 1, "kind": "port",
-            "sample": f"{runs} full integrals by the oracle's sequential restatement (1 thread), {t_total:.1f} s"}
+    return {"value": leaves / t_total, "unit": "accepted subintervals/s", "cores": 1, "host_cpus": ncpu,
+            "kind": "port", "sample": f"{runs} full integrals by the oracle's sequential restatement (1 thread), "
+                                      f"{t_total:.1f} s"}
 
 
 def load_traffic():
@@ -119,6 +113,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # launched by torch.distributed.run (even with one rank): a process group, so the combine below
+    # runs through RCCL; a plain `python bench.py` is the single-GPU run with no group
+    distributed = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
@@ -137,7 +134,7 @@ def main():
     shared = os.environ.get("BENCH_SHARED_GPU") == "1"
     dev = 0 if shared else local_rank
     torch.cuda.set_device(dev)
-    if world > 1:
+    if distributed:
         if shared:
             dist.init_process_group("gloo")
         else:
@@ -145,7 +142,7 @@ def main():
     coll = "cpu" if shared else "cuda"
 
     def all_reduce(t, op):
-        if world > 1:
+        if distributed:
             h = t.to(coll)
             dist.all_reduce(h, op=op)
             if h is not t:
@@ -157,7 +154,7 @@ def main():
     nslots = ctx.async_slots
 
     def barrier():
-        if world > 1:
+        if distributed:
             dist.barrier()
 
     B = args.batch
@@ -223,7 +220,7 @@ def main():
     ctx.kernel_timing(False)
 
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         tt = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
         all_reduce(tt, dist.ReduceOp.MAX)
         elapsed, kern_avg_ms = float(tt[0]), float(tt[1])
@@ -280,7 +277,7 @@ def main():
         }
         print(json.dumps(out))
     ctx.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)

@@ -4,11 +4,15 @@
  * The reference (/root/reference/aquadPartA.c) has no plugin or FFI layer: its boundary is
  * the macro quartet F/A/B/EPSILON (:45-48) plus the farmer/worker message protocol
  * (farmer() :125-173, worker() :175-208) that main() (:78-123) drives. Each entry point below
- * names the reference interface it replaces. Plain C types only: no HIP or torch types cross
- * this boundary; every host buffer is caller-owned; device memory, streams and events are owned
- * by an opaque aq_ctx (one per GPU, not re-entrant, blocking unless the name says _async).
+ * names the reference interface it replaces. Plain C types only: no HIP, RCCL or torch types cross
+ * this boundary; every host buffer is caller-owned; device memory, streams, events and RCCL
+ * communicators are owned by opaque handles (aq_ctx: one GPU; aq_group: GPUs that combine results
+ * over RCCL). No global state; a handle is not re-entrant; calls block unless the name says _async.
  * Errors: 0 on success, a negative AQ_E* code otherwise (the reference's only error is
  * numprocs < 2 -> stderr + exit(1), :86-90; the CLI maps codes to that behaviour).
+ *
+ * Deviation from SURVEY.md §8b's sketch: every call takes its aq_ctx / aq_group first (the sketch's
+ * own "no global state" rule); aq_integrate_batch also returns per-integral task counts.
  */
 #ifndef AQUAD_H
 #define AQUAD_H
@@ -22,41 +26,53 @@ extern "C" {
 #endif
 
 #define AQ_OK 0
-#define AQ_EINVAL (-1)     /* bad argument (non-finite bounds, b < a, eps < 0, bad shard) */
+#define AQ_EINVAL (-1)     /* bad argument (non-finite bounds, b < a, eps < 0, bad shard, outside the integrand's domain) */
 #define AQ_EHIP (-2)       /* a HIP runtime call failed */
-#define AQ_ETIMEOUT (-3)   /* an on-device wait exceeded its bound (never expected) */
+#define AQ_ETIMEOUT (-3)   /* an on-device wait saw no progress for the stall bound (aq_set_stall_timeout) */
 #define AQ_EOVERFLOW (-4)  /* a frontier / work-queue capacity was exceeded */
 #define AQ_EDEPTH (-5)     /* refinement reached max_depth (the reference would not terminate) */
 #define AQ_ENOMEM (-6)     /* device or host allocation failed */
 #define AQ_ENODEV (-7)     /* no HIP device */
+#define AQ_ERCCL (-8)      /* an RCCL call failed (aq_group_*) */
 
 #define AQ_DEFAULT_MAX_DEPTH 96
 #define AQ_MAX_LEVELS 128     /* length of the per-level histograms */
-#define AQ_CU_SLOTS 2048      /* per-CU counter slots: xcc*256 + (se*2+sh)*16 + cu */
+#define AQ_CU_SLOTS 2048      /* hardware CU slot space: xcc*256 + (se*2+sh)*16 + cu */
+#define AQ_XS_LIMBS 68        /* exact area accumulator: int64 limbs (aq_fetch_exact / aq_exact_round) */
+#define AQ_EXACT_ROW (AQ_XS_LIMBS + 4)   /* limbs, tasks, accepted, spilled, levels | error << 32 */
 
 /* Integrand = the reference's F(arg) macro (aquadPartA.c:46) as a compile-time kernel variant. */
 typedef enum {
-    AQ_F_COSH4 = 0,     /* cosh(x)*cosh(x)*cosh(x)*cosh(x), glibc-2.35-exact cosh (the reference) */
-    AQ_F_SIN_RECIP = 1  /* sin(1/x) (SURVEY config 4) */
+    AQ_F_COSH4 = 0,     /* cosh(x)*cosh(x)*cosh(x)*cosh(x), glibc-2.35-exact cosh (the reference), |x| <= 170 */
+    AQ_F_SIN_RECIP = 1, /* sin(1/x) (SURVEY config 4) */
+    AQ_F_USER = 2       /* the plug-in compiled in from AQ_USER_F_HEADER (aq_user_integrand_name()) */
 } aq_integrand;
 
-/* Replaces the compile-time macros EPSILON / F / A / B (aquadPartA.c:45-48). */
+/* Replaces the compile-time macros EPSILON / F / A / B (aquadPartA.c:45-48) and mpirun -n (:83). */
 typedef struct {
     int32_t integrand;  /* aq_integrand */
     int32_t max_depth;  /* refinement cap; 0 -> AQ_DEFAULT_MAX_DEPTH (<= AQ_MAX_LEVELS - 1) */
     double a;           /* A (:47) */
     double b;           /* B (:48) */
     double eps;         /* EPSILON (:45): absolute, strict '>' test (:191) */
+    int32_t n_gpus;     /* GPUs the integral is sharded over: 0 or 1 for aq_integrate, the group size
+                           (or 0) for aq_integrate_group */
+    int32_t reserved;
 } aq_problem;
 
 /* Replaces farmer()'s return value and the global tasks_per_process[] (:72, :101, :162). */
 typedef struct {
-    double area;        /* Σ accepted larea+rarea (:199 sent, :149 summed) */
+    double area;        /* Σ accepted larea+rarea (:199 sent, :149 summed): correctly rounded exact sum */
     uint64_t tasks;     /* intervals evaluated = Σ tasks_per_process (:162) */
     uint64_t accepted;  /* accepted subintervals (tag-1 area messages, :201) */
     uint32_t levels;    /* 1 + deepest refinement level reached */
-    uint32_t n_cu;      /* CUs that evaluated at least one task (aq_tasks_per_cu) */
-    uint64_t spilled;   /* interval records moved through the HBM work queue (load balance) */
+    uint32_t n_cu;      /* CUs that evaluated at least one task (per-CU counts kept: lone-integral launches) */
+    uint64_t spilled;   /* interval pairs moved through the HBM work queue (load balance) */
+    uint32_t n_gpus;    /* GPUs that contributed (entries written to tasks_per_gpu) */
+    uint32_t reserved;
+    uint64_t *tasks_per_gpu;  /* [n_gpus] caller-owned or NULL: tasks per GPU (the workers of :162) */
+    uint64_t *tasks_per_cu;   /* [n_gpus * aq_ctx_num_cus()] caller-owned or NULL: tasks per CU, each
+                                 GPU's CUs in hardware-slot order (0 where not kept) */
 } aq_result;
 
 typedef struct aq_ctx aq_ctx;
@@ -71,34 +87,50 @@ int aq_ctx_num_cus(const aq_ctx *ctx);
 /* Wavefront workers of the on-device farmer (workgroups x waves per workgroup): one integral
  * launched alone is split into this many shares (the partition aq_integrate_shard documents). */
 int aq_ctx_num_workers(const aq_ctx *ctx);
+/* Device memory the context holds, bytes. */
+int aq_ctx_device_bytes(const aq_ctx *ctx, uint64_t *bytes);
 /* Per-level task/accepted histograms on the persistent path (default on; a diagnostic the
  * reference does not produce -- pipelined callers switch it off). */
 int aq_set_level_histograms(aq_ctx *ctx, int enable);
-/* Which persistent kernel runs a launch (no reference counterpart: the reference has one schedule,
- * the MPI bag). AUTO: the lane-DFS kernel for launches of >= 16 integrals, the streaming pair kernel
- * (HBM work queue between CUs) below that. Counts and areas are identical under every engine; the
- * engine only changes the schedule (and aq_ctx_num_workers, the share count of a lone integral).
- * The AQ_ENGINE environment variable ("stream" / "dfs") sets the default of new contexts. */
-#define AQ_ENGINE_AUTO 0
-#define AQ_ENGINE_STREAM 1
-#define AQ_ENGINE_DFS 2
-int aq_set_engine(aq_ctx *ctx, int engine);
+/* How long a waiting workgroup tolerates NO PROGRESS of the on-device work queue before the launch
+ * fails with AQ_ETIMEOUT (default 10 s, or the AQ_STALL_MS environment variable at create time). A
+ * bound on stalls, not on run time: launches of any length that keep progressing never time out. */
+int aq_set_stall_timeout(aq_ctx *ctx, double ms);
+/* Name of the AQ_F_USER plug-in compiled into this library. */
+const char *aq_user_integrand_name(void);
 
 /* ---- the hot path ----------------------------------------------------------------------------
  * aq_integrate: farmer(numprocs) + every worker() of one run (:125-208) as ONE persistent HIP
- * launch: workgroups expand interval frontiers in LDS (task body :183-202), accumulate accepted
+ * launch: wavefronts expand sibling-pair frontiers in LDS (task body :183-202), accumulate accepted
  * areas, and rebalance through an HBM work queue (the bag of tasks, :152-165).
  * Bit-identical interval tree: `tasks` and `accepted` equal the reference's counts exactly.
  */
 int aq_integrate(aq_ctx *ctx, const aq_problem *p, aq_result *res);
 
-/* This process's share of a multi-GPU run: the depth-D positions (D = ceil(log2(V)) + 2) are
+/* This process's share of a multi-GPU run: the depth-D positions (D = floor(log2(V)) + 2) are
  * dealt in snake order over V = nshards * aq_ctx_num_workers() virtual workers; shard `shard`
  * evaluates its positions' subtrees plus the tasks at depth <= D it owns (each counted by the
  * owner of its leftmost descendant position, so by exactly one shard). Summing
- * area/tasks/accepted over all shards (the caller's all-reduce) gives exactly the single-GPU
- * result. */
+ * area/tasks/accepted over all shards (the caller's all-reduce, or aq_integrate_group) gives
+ * exactly the single-GPU result. */
 int aq_integrate_shard(aq_ctx *ctx, const aq_problem *p, int shard, int nshards, aq_result *res);
+
+/* ---- multi-GPU over RCCL (replaces the MPI layer, :145-171, and `result += buff[0]`, :149) ----
+ * A group is a set of contexts, one per GPU, joined by RCCL communicators over xGMI. Either one
+ * process drives n GPUs (aq_group_create: ncclCommInitAll), or every process drives one GPU
+ * (the MPI layout: rank 0 makes an id with aq_group_unique_id, the caller broadcasts it -- e.g.
+ * MPI_Bcast -- and every rank calls aq_group_join). aq_integrate_group runs rank r's shard r of N
+ * on each member, then ONE grouped RCCL exchange: an int64 all-reduce of the exact area limbs and
+ * counts (so the area is the correctly rounded exact sum, whatever N) and an all-gather of each
+ * rank's task / per-CU counts (tasks_per_gpu, tasks_per_cu). Every member gets the whole result. */
+typedef struct aq_group aq_group;
+#define AQ_GROUP_ID_BYTES 128
+int aq_group_create(aq_ctx *const *ctxs, int n, aq_group **out);
+int aq_group_unique_id(void *id /* AQ_GROUP_ID_BYTES */);
+int aq_group_join(aq_ctx *ctx, int nranks, int rank, const void *id, aq_group **out);
+void aq_group_destroy(aq_group *g);
+int aq_group_size(const aq_group *g);
+int aq_integrate_group(aq_group *g, const aq_problem *p, aq_result *res);
 
 /* Asynchronous form for pipelined callers (bench): enqueue one integral on the context's stream,
  * results land in device slot `slot` (0 <= slot < aq_async_slots()); aq_fetch blocks for it. */
@@ -111,19 +143,32 @@ int aq_integrate_async(aq_ctx *ctx, const aq_problem *p, int shard, int nshards,
 int aq_max_integrals_per_launch(void);
 int aq_integrate_many_async(aq_ctx *ctx, int integrand, int k, const double *a, const double *b, double eps,
                             int max_depth, int shard, int nshards, int first_slot);
+/* Like aq_integrate_many_async with a per-integral shard: integral i is shard shard[i] of nshards
+ * (the partition of aq_integrate_shard; every launch of one nshards uses the same partition, so any
+ * rank may run any shard of any integral -- the rebalanced multi-GPU batch, ppls_amd/dist.py). */
+int aq_integrate_mixed_async(aq_ctx *ctx, int integrand, int k, const double *a, const double *b,
+                             const int32_t *shard, int nshards, double eps, int max_depth, int first_slot);
 int aq_fetch(aq_ctx *ctx, int slot, aq_result *res);
+/* The slot's exact row: int64[AQ_EXACT_ROW] = area limbs, tasks, accepted, spilled,
+ * levels | error bits << 32 -- summed limb-wise across shards (an int64 all-reduce), the rounded
+ * area is the same whatever the partition. */
+int aq_fetch_exact(aq_ctx *ctx, int slot, int64_t *row);
+/* Correctly rounded double of AQ_XS_LIMBS exact-accumulator limbs (host function). */
+double aq_exact_round(const int64_t *limbs);
 int aq_synchronize(aq_ctx *ctx);
 /* Enqueue (on the context's stream) a copy of n consecutive slots' totals, starting at first_slot
  * (mod aq_async_slots()), into the DEVICE buffer d_out as n rows of 4 doubles
  * {area, tasks, accepted, error bits}: the input of one all-reduce for n pipelined integrals. */
 int aq_gather_results(aq_ctx *ctx, int first_slot, int n, void *d_out);
+/* The same slots as exact int64 rows (AQ_EXACT_ROW each) into the DEVICE buffer d_out. */
+int aq_gather_exact(aq_ctx *ctx, int first_slot, int n, void *d_out);
 
 /* Level-synchronous breadth-first path (one kernel per tree level, host loop): the debug /
  * cross-check schedule. Fills per-level histograms (caller arrays of length maxlev or NULL). */
 int aq_integrate_levels(aq_ctx *ctx, const aq_problem *p, aq_result *res, uint64_t *tasks_per_level,
                         uint64_t *leaves_per_level, int maxlev);
 
-/* Frontier engine over caller-owned device buffers (the multi-GPU rebalanced schedule of
+/* Frontier engine over caller-owned device buffers (the level-synchronous multi-GPU schedule of
  * ppls_amd/frontier.py). A frontier is n records {l, r, F(l), F(r)} (4 doubles each, row-major) of
  * one tree depth. aq_frontier_root writes the root record of [a, b] to d_out[0].
  * aq_level_step enqueues one task step (aquadPartA.c:183-202) on every record of d_in: refining
@@ -144,9 +189,9 @@ int aq_level_histogram(aq_ctx *ctx, uint64_t *tasks_per_level, uint64_t *leaves_
 int aq_tasks_per_cu(aq_ctx *ctx, uint64_t *out, int cap);
 
 /* Batch front end (SURVEY config 3): n independent integrals [a[i], b[i]] of one integrand.
- * Per-integral area / tasks / accepted (any may be NULL). */
-int aq_integrate_batch(aq_ctx *ctx, int integrand, size_t n, const double *a, const double *b, double eps,
-                       double *area, uint64_t *tasks, uint64_t *accepted);
+ * Per-integral area / accepted / tasks (any may be NULL). */
+int aq_integrate_batch(aq_ctx *ctx, size_t n, const double *a, const double *b, double eps, int integrand,
+                       double *area, uint64_t *accepted, uint64_t *tasks);
 
 /* Device evaluation of the integrand / of cosh (libm parity checks). */
 int aq_eval_integrand(aq_ctx *ctx, int integrand, size_t n, const double *x, double *out);
@@ -167,9 +212,13 @@ int aq_set_diagnostics(aq_ctx *ctx, int enable);
 int aq_diagnostics(aq_ctx *ctx, uint64_t *out, int cap_words);
 
 /* ---- observable surface ----------------------------------------------------------------------
- * Prints exactly main()'s output (:107-117): "Area=%lf\n\nTasks Per Process\n", then the index
- * row and the count row, each entry followed by a tab. Entry 0 is the farmer (always 0). */
-void aq_print_reference(FILE *f, double area, const uint64_t *tasks_per_process, int nprocs);
+ * aq_print_reference prints exactly main()'s output (:107-117) for a result: "Area=%lf\n\nTasks Per
+ * Process\n", then the index row and the count row, each entry followed by a tab. Entry 0 is the
+ * farmer (always 0), entries 1..n_gpus the GPUs' tasks (res->tasks_per_gpu; one worker when NULL).
+ * aq_print_reference_procs prints the same for any tasks_per_process[nprocs] (e.g. CUs dealt over
+ * P-1 worker columns, the CLI's `-n P`). */
+void aq_print_reference(FILE *f, const aq_result *res);
+void aq_print_reference_procs(FILE *f, double area, const uint64_t *tasks_per_process, int nprocs);
 
 #ifdef __cplusplus
 }

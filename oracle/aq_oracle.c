@@ -37,6 +37,7 @@
 /* integrand ids: same numbering as include/aquad.h */
 #define AQO_F_COSH4 0     /* aquadPartA.c:46 */
 #define AQO_F_SIN_RECIP 1 /* sin(1/x): the SURVEY config-4 variant of the F macro */
+#define AQO_F_USER 2      /* exp(-(arg)*(arg)): the library's default AQ_F_USER plug-in (the macro at :46 replaced) */
 
 static inline uint64_t asu(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
 static inline double asd(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
@@ -51,56 +52,72 @@ static const double C3 = 0x1.555555555543cp-3;
 static const double C4 = 0x1.55555cf172b91p-5;
 static const double C5 = 0x1.1111167a4d017p-7;
 
-/* FMA ifunc form (__exp_fma): GCC contracts z+Shift, r, tmp and scale+scale*tmp. */
-double aqo_exp_fma(double x)
+/*
+ * Both ifunc forms of glibc's __exp (e_exp.c), every path: |x| < 2^-54 -> 1 + x; |x| >= 1024 ->
+ * 0 / inf / nan; otherwise the N=128 table evaluation, with specialcase() for |x| >= 512 (k > 0:
+ * overflow-safe scaling; k < 0: the subnormal range with its hi/lo re-rounding). The FMA form
+ * (__exp_fma, what x86_64 hosts with FMA select) is GCC's contraction of the same source:
+ * z+Shift, r, tmp, scale+scale*tmp and scale-y+scale*tmp fuse; this file itself builds with
+ * -ffp-contract=off, so the non-FMA form below is the source as written.
+ */
+static double exp_any(double x, int fma_variant)
 {
     uint32_t abstop = (uint32_t)(asu(x) >> 52) & 0x7ff;
-    int large = abstop >= 0x408; /* |x| >= 512: glibc's specialcase() */
-    if (abstop >= 0x409 && x > 0x1.62e42fefa39efp+9) return INFINITY;
-    double kd = fma(InvLn2N, x, Shift);
+    int special = 0;
+    if (abstop - 0x3c9u >= 0x408u - 0x3c9u) {
+        if ((int32_t)(abstop - 0x3c9u) < 0) return 1.0 + x;       /* tiny */
+        if (abstop >= 0x409) {                                     /* |x| >= 1024 */
+            if (asu(x) == asu(-INFINITY)) return 0.0;
+            if (abstop >= 0x7ff) return 1.0 + x;
+            return (asu(x) >> 63) ? 0.0 : INFINITY;
+        }
+        special = 1;
+    }
+    double kd, r;
+    if (fma_variant) {
+        kd = fma(InvLn2N, x, Shift);
+    } else {
+        double z = InvLn2N * x;
+        kd = z + Shift;
+    }
     uint64_t ki = asu(kd);
     kd -= Shift;
-    double r = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x));
+    if (fma_variant) r = fma(kd, NegLn2loN, fma(kd, NegLn2hiN, x));
+    else r = x + kd * NegLn2hiN + kd * NegLn2loN;
     uint64_t idx = 2 * (ki % 128);
     uint64_t top = ki << 45;
     double tail = asd(aqo_exp_tab[idx]);
     uint64_t sbits = aqo_exp_tab[idx + 1] + top;
     double r2 = r * r;
-    double tmp = fma(r2 * r2, fma(r, C5, C4), fma(r2, fma(r, C3, C2), tail + r));
-    if (large) { /* specialcase, k > 0 branch */
-        sbits -= 1009ull << 52;
+    double tmp;
+    if (fma_variant) tmp = fma(r2 * r2, fma(r, C5, C4), fma(r2, fma(r, C3, C2), tail + r));
+    else tmp = tail + r + r2 * (C2 + r * C3) + r2 * r2 * (C4 + r * C5);
+    if (special) {
+        if ((ki & 0x80000000ull) == 0) {                           /* k > 0 */
+            sbits -= 1009ull << 52;
+            double scale = asd(sbits);
+            return 0x1p1009 * (fma_variant ? fma(scale, tmp, scale) : scale + scale * tmp);
+        }
+        /* k < 0: GCC leaves this branch unfused in the FMA form too (measured against the host
+           libm: fusing either line gives 28 / 254 mismatches in 2 M points, unfused 0) */
+        sbits += 1022ull << 52;
         double scale = asd(sbits);
-        return 0x1p1009 * fma(scale, tmp, scale);
+        double y = scale + scale * tmp;
+        if (y < 1.0) {
+            double lo = scale - y + scale * tmp;
+            double hi = 1.0 + y;
+            lo = 1.0 - hi + y + lo;
+            y = (hi + lo) - 1.0;
+            if (y == 0.0) y = 0.0;
+        }
+        return 0x1p-1022 * y;
     }
     double scale = asd(sbits);
-    return fma(scale, tmp, scale);
+    return fma_variant ? fma(scale, tmp, scale) : scale + scale * tmp;
 }
 
-/* Non-FMA ifunc form (__exp_sse2): same source, no contraction (this file: -ffp-contract=off). */
-double aqo_exp_nofma(double x)
-{
-    uint32_t abstop = (uint32_t)(asu(x) >> 52) & 0x7ff;
-    int large = abstop >= 0x408;
-    if (abstop >= 0x409 && x > 0x1.62e42fefa39efp+9) return INFINITY;
-    double z = InvLn2N * x;
-    double kd = z + Shift;
-    uint64_t ki = asu(kd);
-    kd -= Shift;
-    double r = x + kd * NegLn2hiN + kd * NegLn2loN;
-    uint64_t idx = 2 * (ki % 128);
-    uint64_t top = ki << 45;
-    double tail = asd(aqo_exp_tab[idx]);
-    uint64_t sbits = aqo_exp_tab[idx + 1] + top;
-    double r2 = r * r;
-    double tmp = tail + r + r2 * (C2 + r * C3) + r2 * r2 * (C4 + r * C5);
-    if (large) {
-        sbits -= 1009ull << 52;
-        double scale = asd(sbits);
-        return 0x1p1009 * (scale + scale * tmp);
-    }
-    double scale = asd(sbits);
-    return scale + scale * tmp;
-}
+double aqo_exp_fma(double x) { return exp_any(x, 1); }
+double aqo_exp_nofma(double x) { return exp_any(x, 0); }
 
 /* ---- glibc 2.35 expm1, s_expm1.c, the |x| < 0.5*ln2 (k = 0) path ----------------------- */
 static const double Q1 = -3.33333333333331316428e-02;
@@ -161,6 +178,11 @@ double aqo_cosh(double x, int fma_variant)
 static inline double F_eval(int integrand, int mode, double x)
 {
     if (integrand == AQO_F_SIN_RECIP) return sin(1.0 / x);
+    if (integrand == AQO_F_USER) {
+        double y = -x * x;                  /* the macro expands to -(arg)*(arg) = (-x)*x */
+        if (mode == AQO_LIBM_HOST) return exp(y);
+        return mode == AQO_LIBM_RESTATED_FMA ? aqo_exp_fma(y) : aqo_exp_nofma(y);
+    }
     double c;
     if (mode == AQO_LIBM_HOST) c = cosh(x);
     else c = aqo_cosh(x, mode == AQO_LIBM_RESTATED_FMA);

@@ -17,6 +17,7 @@ REF_DIR = os.path.join(HERE, "_ref")
 
 COSH4 = 0
 SIN_RECIP = 1
+USER = 2        # exp(-x*x): the library's default AQ_F_USER plug-in
 
 RESTATED_FMA = 0
 RESTATED_NOFMA = 1

@@ -6,13 +6,20 @@ the same accepted-interval count, area and `Area=` / `Tasks Per Process` printou
 hand-written HIP kernels for gfx950 behind the C ABI in include/aquad.h.
 """
 from .aquad import (  # noqa: F401
+    COSH4,
+    SIN_RECIP,
+    USER,
     AquadError,
     Context,
+    Group,
     Problem,
     Result,
+    exact_round,
     farmer,
     format_reference,
     integrate,
+    user_integrand_name,
 )
 
-__all__ = ["AquadError", "Context", "Problem", "Result", "farmer", "format_reference", "integrate"]
+__all__ = ["COSH4", "SIN_RECIP", "USER", "AquadError", "Context", "Group", "Problem", "Result", "exact_round",
+           "farmer", "format_reference", "integrate", "user_integrand_name"]

@@ -17,7 +17,8 @@ from . import _lib
 
 COSH4 = 0
 SIN_RECIP = 1
-INTEGRANDS = {"cosh4": COSH4, "sin_recip": SIN_RECIP}
+USER = 2        # the AQ_F_USER plug-in compiled into the library (default: exp(-x*x))
+INTEGRANDS = {"cosh4": COSH4, "sin_recip": SIN_RECIP, "user": USER}
 
 # aquadPartA.c:45-48
 DEFAULT_EPSILON = 1e-3
@@ -40,10 +41,12 @@ class Problem:
     b: float = DEFAULT_B
     eps: float = DEFAULT_EPSILON
     max_depth: int = 0
+    n_gpus: int = 0
 
     def c(self):
         f = self.integrand if isinstance(self.integrand, int) else INTEGRANDS[self.integrand]
-        return _lib.aq_problem(f, int(self.max_depth), float(self.a), float(self.b), float(self.eps))
+        return _lib.aq_problem(f, int(self.max_depth), float(self.a), float(self.b), float(self.eps),
+                               int(self.n_gpus), 0)
 
 
 @dataclass
@@ -57,6 +60,7 @@ class Result:
     tasks_per_cu: Dict[int, int] = field(default_factory=dict)
     tasks_per_level: List[int] = field(default_factory=list)
     leaves_per_level: List[int] = field(default_factory=list)
+    tasks_per_gpu: List[int] = field(default_factory=list)
 
 
 def _check(rc, what):
@@ -71,6 +75,16 @@ def _dp(a):
 
 def _up(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def exact_round(limbs) -> float:
+    """Correctly rounded double of AQ_XS_LIMBS exact-accumulator limbs (e.g. summed over shards)."""
+    v = np.ascontiguousarray(np.asarray(limbs)[:_lib.AQ_XS_LIMBS], np.int64)
+    return _lib.load().aq_exact_round(v.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+
+
+def user_integrand_name() -> str:
+    return _lib.load().aq_user_integrand_name().decode()
 
 
 def device_count() -> int:
@@ -89,16 +103,21 @@ class Context:
         self.device = device
         self.num_cus = self.L.aq_ctx_num_cus(self._h)
 
-    ENGINES = {"auto": 0, "stream": 1, "dfs": 2}
-
     @property
     def num_workers(self) -> int:
-        """Shares a lone integral is split into under the current engine (the oracle partition's G)."""
+        """Shares a lone integral is split into (the oracle partition's G): workgroups x waves."""
         return self.L.aq_ctx_num_workers(self._h)
 
-    def set_engine(self, engine: str):
-        """Persistent kernel for later launches: "auto", "stream" (pair rings + HBM queue) or "dfs" (lane DFS)."""
-        _check(self.L.aq_set_engine(self._h, self.ENGINES[engine]), "aq_set_engine")
+    @property
+    def device_bytes(self) -> int:
+        """Device memory this context holds."""
+        v = ctypes.c_uint64(0)
+        _check(self.L.aq_ctx_device_bytes(self._h, ctypes.byref(v)), "aq_ctx_device_bytes")
+        return v.value
+
+    def set_stall_timeout(self, ms: float):
+        """Fail a launch whose on-device work queue makes no progress for `ms` (not a run-time cap)."""
+        _check(self.L.aq_set_stall_timeout(self._h, float(ms)), "aq_set_stall_timeout")
 
     def close(self):
         if self._h:
@@ -123,6 +142,7 @@ class Context:
     # -- results ---------------------------------------------------------------------------
     def _result(self, r, with_detail=True) -> Result:
         out = Result(r.area, int(r.tasks), int(r.accepted), int(r.levels), int(r.n_cu), int(r.spilled))
+        out.tasks_per_gpu = [int(r.tasks)]
         if with_detail:
             cu = np.zeros(_lib.AQ_CU_SLOTS, np.uint64)
             self.L.aq_tasks_per_cu(self._h, _up(cu), _lib.AQ_CU_SLOTS)
@@ -175,10 +195,30 @@ class Context:
         _check(self.L.aq_integrate_many_async(self._h, integrand, a.size, _dp(a), _dp(b), float(eps), max_depth,
                                               shard, nshards, first_slot), "aq_integrate_many_async")
 
+    def integrate_mixed_async(self, a, b, shards, nshards, eps, first_slot=0, integrand=COSH4, max_depth=0):
+        """One launch of len(a) integral shards: integral i is shard shards[i] of nshards."""
+        a = np.ascontiguousarray(a, np.float64)
+        b = np.ascontiguousarray(b, np.float64)
+        sh = np.ascontiguousarray(shards, np.int32)
+        _check(self.L.aq_integrate_mixed_async(self._h, integrand, a.size, _dp(a), _dp(b),
+                                               sh.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(nshards),
+                                               float(eps), max_depth, first_slot), "aq_integrate_mixed_async")
+
     def fetch(self, slot: int, detail=False) -> Result:
         r = _lib.aq_result()
         _check(self.L.aq_fetch(self._h, slot, ctypes.byref(r)), "aq_fetch")
         return self._result(r, with_detail=detail)
+
+    def fetch_exact(self, slot: int) -> np.ndarray:
+        """The slot's exact row: int64[AQ_EXACT_ROW] = area limbs, tasks, accepted, spilled, levels | error << 32."""
+        row = np.zeros(_lib.AQ_EXACT_ROW, np.int64)
+        _check(self.L.aq_fetch_exact(self._h, slot, row.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))),
+               "aq_fetch_exact")
+        return row
+
+    def gather_exact(self, first_slot: int, n: int, device_ptr: int):
+        """Enqueue n slots' exact int64 rows (AQ_EXACT_ROW each) into a device buffer."""
+        _check(self.L.aq_gather_exact(self._h, first_slot, n, ctypes.c_void_p(device_ptr)), "aq_gather_exact")
 
     def gather_results(self, first_slot: int, n: int, device_ptr: int):
         """Enqueue slots' {area, tasks, accepted, error} rows into a device buffer (e.g. a torch tensor)."""
@@ -223,8 +263,8 @@ class Context:
         area = np.empty(n, np.float64)
         tasks = np.empty(n, np.uint64)
         acc = np.empty(n, np.uint64)
-        _check(self.L.aq_integrate_batch(self._h, integrand, n, _dp(a), _dp(b), float(eps), _dp(area), _up(tasks),
-                                         _up(acc)), "aq_integrate_batch")
+        _check(self.L.aq_integrate_batch(self._h, n, _dp(a), _dp(b), float(eps), integrand, _dp(area), _up(acc),
+                                         _up(tasks)), "aq_integrate_batch")
         return area, tasks, acc
 
     def eval_cosh(self, x):
@@ -238,6 +278,70 @@ class Context:
         out = np.empty_like(x)
         _check(self.L.aq_eval_integrand(self._h, integrand, x.size, _dp(x), _dp(out)), "aq_eval_integrand")
         return out
+
+
+class Group:
+    """GPUs that combine one integral's shards over RCCL (aq_group): one process driving several
+    contexts (Group([ctx0, ctx1, ...])), or one process per GPU (Group.join(ctx, nranks, rank, uid)
+    with uid = Group.unique_id() from rank 0, broadcast by the caller)."""
+
+    def __init__(self, contexts=None, _handle=None):
+        self.L = _lib.load()
+        self._h = ctypes.c_void_p()
+        self.contexts = list(contexts or [])
+        if _handle is not None:
+            self._h = _handle
+        else:
+            arr = (ctypes.c_void_p * len(self.contexts))(*[c._h.value for c in self.contexts])
+            _check(self.L.aq_group_create(arr, len(self.contexts), ctypes.byref(self._h)), "aq_group_create")
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(_lib.AQ_GROUP_ID_BYTES)
+        _check(_lib.load().aq_group_unique_id(buf), "aq_group_unique_id")
+        return buf.raw
+
+    @classmethod
+    def join(cls, ctx, nranks: int, rank: int, uid: bytes):
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), _lib.AQ_GROUP_ID_BYTES)
+        _check(L.aq_group_join(ctx._h, int(nranks), int(rank), buf, ctypes.byref(h)), "aq_group_join")
+        return cls([ctx], _handle=h)
+
+    @property
+    def size(self) -> int:
+        return self.L.aq_group_size(self._h)
+
+    def integrate(self, problem: "Problem") -> Result:
+        n = self.size
+        ncu = self.contexts[0].num_cus
+        per_gpu = np.zeros(n, np.uint64)
+        per_cu = np.zeros(n * ncu, np.uint64)
+        r = _lib.aq_result()
+        r.tasks_per_gpu = _up(per_gpu)
+        r.tasks_per_cu = _up(per_cu)
+        _check(self.L.aq_integrate_group(self._h, ctypes.byref(problem.c()), ctypes.byref(r)), "aq_integrate_group")
+        out = Result(r.area, int(r.tasks), int(r.accepted), int(r.levels), int(r.n_cu), int(r.spilled))
+        out.tasks_per_gpu = [int(v) for v in per_gpu]
+        out.tasks_per_cu = {(g, k): int(per_cu[g * ncu + k]) for g in range(n) for k in range(ncu) if per_cu[g * ncu + k]}
+        t = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+        lv = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+        self.L.aq_level_histogram(self.contexts[0]._h, _up(t), _up(lv), _lib.AQ_MAX_LEVELS)
+        out.tasks_per_level = [int(v) for v in t[:out.levels]]
+        out.leaves_per_level = [int(v) for v in lv[:out.levels]]
+        return out
+
+    def close(self):
+        if self._h:
+            self.L.aq_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def integrate(integrand="cosh4", a=DEFAULT_A, b=DEFAULT_B, eps=DEFAULT_EPSILON, device=0, ctx=None) -> Result:

@@ -24,8 +24,13 @@ HIP_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 SOURCES = [os.path.join(CSRC, "aquad.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_device.h", "aq_stream.h", "aq_dfs.h")] + \
-    [os.path.join(ROOT, "include", "aquad.h")]
+# AQ_F_USER plug-in header (the reference's F(arg) macro, aquadPartA.c:46): the default Gaussian,
+# or any header named by PPLS_AMD_USER_F (see csrc/plugins/aq_user_gauss.h for the interface)
+USER_F = os.path.abspath(os.environ.get("PPLS_AMD_USER_F") or os.path.join(CSRC, "plugins", "aq_user_gauss.h"))
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_device.h", "aq_stream.h",
+                                                  "aq_xsum.h", "aq_abi.inc")] + \
+    [os.path.join(ROOT, "include", "aquad.h"), USER_F]
+LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _stale(target, deps):
@@ -41,7 +46,7 @@ def build(force=False, verbose=False):
     if not os.path.exists(tab):
         subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_exp_table.py")])
     if force or _stale(LIB, DEPS):
-        cmd = [HIPCC] + HIP_FLAGS + ["-o", LIB] + SOURCES
+        cmd = [HIPCC] + HIP_FLAGS + [f'-DAQ_USER_F_HEADER="{USER_F}"', "-o", LIB] + SOURCES + LIBS
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)

@@ -79,6 +79,16 @@ struct Step2 {
     double fmid, area2;   // F(mid) and 2 * (larea + rarea)
     bool refine;
 };
+//
+// Doubling needs every product to stay normal: the built-in integrands guarantee it on their
+// validated domains (aq_abi.inc bounds_ok). A plug-in F (F_USER) can be anything, so its trees use
+// the reference's expressions literally, '/2' included: area2 is then the plain larea + rarea and
+// the caller passes eps itself (area_scale<FID>() says which).
+template <int FID>
+__host__ __device__ constexpr bool doubled_areas() { return FID != F_USER; }
+template <int FID>
+__host__ __device__ constexpr double area_scale() { return doubled_areas<FID>() ? 0.5 : 1.0; }
+
 template <int FID, int K>
 __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (&r)[K], const double (&fl)[K],
                                             const double (&fr)[K], double eps2, const ExpEntry* __restrict__ tab,
@@ -89,12 +99,21 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
     integrand_k<FID, K>(mid, fmid, tab, kk, range_hint);       // :188
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const double lr2 = (fl[k] + fr[k]) * (r[k] - l[k]);           // 2 * lrarea, :185
-        const double l2 = (fl[k] + fmid[k]) * (mid[k] - l[k]);        // 2 * larea,  :189
-        const double r2 = (fmid[k] + fr[k]) * (r[k] - mid[k]);        // 2 * rarea,  :190
-        s[k].fmid = fmid[k];
-        s[k].area2 = l2 + r2;
-        s[k].refine = fabs(s[k].area2 - lr2) > eps2;                  // :191 (strict >)
+        if constexpr (doubled_areas<FID>()) {
+            const double lr2 = (fl[k] + fr[k]) * (r[k] - l[k]);           // 2 * lrarea, :185
+            const double l2 = (fl[k] + fmid[k]) * (mid[k] - l[k]);        // 2 * larea,  :189
+            const double r2 = (fmid[k] + fr[k]) * (r[k] - mid[k]);        // 2 * rarea,  :190
+            s[k].fmid = fmid[k];
+            s[k].area2 = l2 + r2;
+            s[k].refine = fabs(s[k].area2 - lr2) > eps2;                  // :191 (strict >)
+        } else {   // eps2 is eps here (area_scale 1)
+            const double lrarea = (fl[k] + fr[k]) * (r[k] - l[k]) / 2;    // :185
+            const double larea = (fl[k] + fmid[k]) * (mid[k] - l[k]) / 2; // :189
+            const double rarea = (fmid[k] + fr[k]) * (r[k] - mid[k]) / 2; // :190
+            s[k].fmid = fmid[k];
+            s[k].area2 = larea + rarea;                                   // :199
+            s[k].refine = fabs((larea + rarea) - lrarea) > eps2;          // :191 (strict >)
+        }
     }
 }
 

@@ -68,6 +68,54 @@ __device__ __forceinline__ double exp_glibc(double x, const ExpEntry* __restrict
     return __fma_rn(scale, tmp, scale);
 }
 
+// glibc __exp (e_exp.c, FMA ifunc form) for every double: the tiny-argument path (|x| < 2^-54:
+// 1 + x), the main path, and both specialcase() branches (k > 0: |x| >= 512 overflow scaling; k < 0:
+// the subnormal range with its hi/lo re-rounding). Plug-in integrands (AQ_F_USER) call this one.
+__device__ __forceinline__ double exp_glibc_any(double x, const ExpEntry* __restrict__ tab) {
+    const uint32_t abstop = (uint32_t)((uint64_t)__double_as_longlong(x) >> 52) & 0x7ffu;
+    bool special = false;
+    if (__builtin_expect(abstop - 0x3c9u >= 0x408u - 0x3c9u, 0)) {   // |x| < 2^-54 or |x| >= 512 (or nan / inf)
+        if ((int)(abstop - 0x3c9u) < 0) return 1.0 + x;
+        if (abstop >= 0x409u) {                                        // |x| >= 1024
+            if (__double_as_longlong(x) == (long long)0xfff0000000000000ull) return 0.0;
+            if (abstop >= 0x7ffu) return 1.0 + x;
+            return x < 0.0 ? 0.0 : __longlong_as_double(0x7ff0000000000000LL);
+        }
+        special = true;
+    }
+    double kd = __fma_rn(kInvLn2N, x, kShift);
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd = kd - kShift;
+    const double r = __fma_rn(kd, kNegLn2loN, __fma_rn(kd, kNegLn2hiN, x));
+    const ExpEntry e = tab[ki & 127];
+    const double tail = __longlong_as_double((long long)e.tail_bits);
+    uint64_t sbits = e.sbits + (ki << 45);
+    const double r2 = r * r;
+    const double tmp = __fma_rn(r2 * r2, __fma_rn(r, kC5, kC4), __fma_rn(r2, __fma_rn(r, kC3, kC2), tail + r));
+    if (__builtin_expect(special, 0)) {
+        if ((ki & 0x80000000ull) == 0) {                               // k > 0
+            sbits -= 1009ull << 52;
+            const double scale = __longlong_as_double((long long)sbits);
+            return 0x1p1009 * __fma_rn(scale, tmp, scale);
+        }
+        // k < 0, the subnormal range: glibc's FMA build leaves this branch unfused (checked against
+        // the host libm, oracle/aq_oracle.c exp_any)
+        sbits += 1022ull << 52;
+        const double scale = __longlong_as_double((long long)sbits);
+        double y = scale + scale * tmp;
+        if (y < 1.0) {
+            double lo = scale - y + scale * tmp;
+            const double hi = 1.0 + y;
+            lo = 1.0 - hi + y + lo;
+            y = (hi + lo) - 1.0;
+            if (y == 0.0) y = 0.0;
+        }
+        return 0x1p-1022 * y;
+    }
+    const double scale = __longlong_as_double((long long)sbits);
+    return __fma_rn(scale, tmp, scale);
+}
+
 // glibc __expm1 for |x| < 0.5*ln2 (the only range cosh passes it).
 __device__ __forceinline__ double expm1_glibc_small(double x) {
     if ((hi_word(x) & 0x7fffffffu) < 0x3c900000u) return x;
@@ -139,7 +187,25 @@ __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restric
 }
 
 // Integrand ids (include/aquad.h aq_integrand).
-enum : int { F_COSH4 = 0, F_SIN_RECIP = 1 };
+enum : int { F_COSH4 = 0, F_SIN_RECIP = 1, F_USER = 2 };
+
+}  // namespace aq
+
+// The AQ_F_USER plug-in: the reference's extension point is the F(arg) macro (aquadPartA.c:46);
+// here a header, chosen at build time with -DAQ_USER_F_HEADER=<file> (ppls_amd/build.py:
+// PPLS_AMD_USER_F=<file>), defines in namespace aq::user
+//   constexpr const char* name;                                  -- reported by aq_user_integrand_name()
+//   __device__ double F(double x, const aq::ExpEntry* tab);      -- the macro body (tab: LDS exp table
+//                                                                   for aq::exp_glibc_any / cosh_glibc)
+//   inline bool domain_ok(double a, double b);                   -- host check of [a, b]
+// and is compiled into every kernel as integrand id 2. Plug-in trees use the reference's own area
+// expressions literally (no doubled-area rescaling), so they are bit-exact for any finite F.
+#ifndef AQ_USER_F_HEADER
+#define AQ_USER_F_HEADER "plugins/aq_user_gauss.h"
+#endif
+#include AQ_USER_F_HEADER
+
+namespace aq {
 
 // F(arg) exactly as the reference macro expands (aquadPartA.c:46): ((c*c)*c)*c.
 template <int FID>
@@ -147,6 +213,8 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
     if constexpr (FID == F_COSH4) {
         const double c = cosh_glibc(x, tab);
         return c * c * c * c;
+    } else if constexpr (FID == F_USER) {
+        return user::F(x, tab);
     } else {
         // SURVEY config 4: sin(1/x). Leaf counts are insensitive to +-1 ulp in sin,
         // so the device libm's faithful sin is used.
@@ -265,6 +333,9 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) f[k] = c[k] * c[k] * c[k] * c[k];
+    } else if constexpr (FID == F_USER) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) f[k] = user::F(x[k], tab);
     } else {
 #pragma unroll
         for (int k = 0; k < K; ++k) f[k] = sin(1.0 / x[k]);

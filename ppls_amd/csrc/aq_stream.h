@@ -2,10 +2,11 @@
 //
 // Reference: /root/reference/aquadPartA.c. The farmer's LIFO bag (:125-173) and the workers' task
 // body (:183-202) become one persistent launch:
-//   * the unit of work is a SIBLING PAIR {a, m, b, F(a), F(m), F(b), depth | integral<<8}
-//     = the two tasks [a,m] and [m,b] a refining parent pushes (:192-197). A pair is 52 bytes for two
-//     tasks (two separate records would be 72), and it hands every lane two independent
-//     evaluations: the K=2 cosh chains interleave (aq_libm.h cosh_main_k).
+//   * the unit of work is a SIBLING PAIR {a, b, F(a), F(m), F(b), depth | integral<<8}
+//     = the two tasks [a,m] and [m,b] a refining parent pushes (:192-197); m = (a+b)/2 is recomputed
+//     from the parent's own operands (:187), so it is not stored. A pair is 44 bytes for two tasks
+//     (two separate records would be 72), and it hands every lane two independent evaluations: the
+//     K=2 cosh chains interleave (aq_libm.h cosh_main_k).
 //   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of pairs. A round pops
 //     <= 64 pairs, evaluates F at both midpoints in FP64 (glibc-exact cosh), applies the reference's
 //     refine test (:191) to both tasks and pushes each refining task's children as a new pair, with a
@@ -24,12 +25,14 @@
 //     so the tail of one integral overlaps the start of the next, and waves that draw light shares
 //     take more of them.
 //   * accepted areas / task counts accumulate per lane in registers per integral and are flushed
-//     (wave reduction + one set of uncontended atomics into this workgroup's partial of that
-//     integral) when a wave switches integral or exits (the farmer's `result += buff[0]`, :149).
+//     (wave reduction + a few device atomics into the integral's slot: counts, and the area into an
+//     exact fixed-point accumulator, aq_xsum.h) when a wave switches integral or exits (the
+//     farmer's `result += buff[0]`, :149).
 // Every decision is the reference's own arithmetic on the same operands, so the interval tree --
 // tasks and accepted counts -- is bit-identical whatever the schedule.
 #pragma once
 #include "aq_device.h"
+#include "aq_xsum.h"
 
 namespace aq {
 
@@ -83,21 +86,20 @@ constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches
 #endif
 constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch (13 VGPRs)
 
-// Queue control block (HBM ticket queue) and per-integral histogram accumulators. One per async
-// slot; it must be all-zero when a launch starts -- the host zeroes slots lazily in batches.
+// Queue control block (HBM ticket queue), per-integral totals and histogram accumulators. One per
+// async slot; it must be all-zero when a launch starts -- the host zeroes slots lazily in batches.
 // q_tokens stores (tokens - G): the protocol's token count starts at G (every workgroup busy) and
 // the run is over when it reaches 0. jobs counts claimed jobs beyond the first W.
 struct alignas(128) Line {
     unsigned v;
     unsigned pad[31];
 };
-// Per-integral totals (device-scope atomics at every flush) and the list of waves that flushed an
-// area partial into the slot: gathers and resets read only those partials, not all 4096 of them
-// (a list longer than TCAP falls back to the dense pass).
-constexpr unsigned TCAP = 224;
+// Per-integral totals: device-scope atomics at every flush (the farmer's `result += buff[0]`, :149,
+// and tasks_per_process, :162). The area is the exact fixed-point sum of the waves' double-double
+// partials (aq_xsum.h): order-independent, rounded once when it is read.
 struct alignas(128) SlotSums {
     unsigned long long tasks, leaves, spilled;
-    unsigned levels, error, ntouch, pad;
+    unsigned levels, error;
 };
 struct Ctl {
     Line q_tail;               // chunk slots claimed by producers
@@ -105,22 +107,25 @@ struct Ctl {
     Line q_tokens;             // tokens - G
     Line jobs;                 // job claims
     SlotSums sums;
-    unsigned touch[TCAP];      // waves with a partial in this slot (repeats possible)
+    XSum area;                 // exact Σ of the accepted areas (larea + rarea, :199)
     unsigned long long hist[2 * AQ_MAX_LEVELS];   // [0,L): tasks per level, [L,2L): accepted per level
 };
 
-// One workgroup's share of one integral, accumulated with uncontended atomics (zeroed per slot).
-// Its area lives in the per-wave double-double partials (StreamParams::warea), not here.
-struct WgPart {
-    unsigned long long spare;
-    unsigned long long tasks;
-    unsigned long long leaves;
-    unsigned long long spilled;   // pairs this workgroup moved through the HBM queue (slot first_slot)
-    unsigned levels;
-    unsigned error;
-    unsigned cu;                  // hardware CU slot
-    unsigned pad;
-};
+// Per-CU task counts of lone-integral (per-CU) launches: one word per (slot, workgroup), written once
+// by the workgroup's last wave: tasks << CU_BITS | hardware CU slot.
+constexpr int CU_BITS = 11;   // AQ_CU_SLOTS = 2048
+__host__ __device__ __forceinline__ unsigned long long pack_cu(unsigned long long tasks, unsigned cu) {
+    return (tasks << CU_BITS) | (unsigned long long)(cu & ((1u << CU_BITS) - 1u));
+}
+
+// Exact accumulation into a slot's XSum (device atomics: any order, same bits).
+__device__ __forceinline__ void xs_atomic_add(long long* limbs, double x) {
+    XDigits g;
+    if (!xs_digits(x, g)) return;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (g.d[k]) atomicAdd(reinterpret_cast<unsigned long long*>(&limbs[g.i + k]), (unsigned long long)g.d[k]);
+}
 
 struct Chunk {                      // SoA, one queue slot
     double a[CH], b[CH], fa[CH], fm[CH], fb[CH];
@@ -132,7 +137,8 @@ struct Chunk {                      // SoA, one queue slot
 // A wave's private HBM overflow stack: the bottom (oldest, shallowest) pairs of a full ring go
 // down here without any lock; the wave takes them back when its ring runs dry, before it looks at
 // the shared pool or seeds new work, so the cellar is empty whenever the wave reports idle. Only
-// the owning wave touches it (one CU, one L2), so it stays on-die.
+// the owning wave touches it; its lines are written back to HBM when the L2 evicts them (the PMC
+// passes measure ~13 GB of WRITE_SIZE per 8192-integral launch).
 struct Cellar {
     double a[CCAP], b[CCAP], fa[CCAP], fm[CCAP], fb[CCAP];
     unsigned dt[CCAP];
@@ -149,6 +155,7 @@ struct alignas(128) LaunchHint {
 
 struct StreamParams {
     const double2* bounds;          // [nprob] {a, b} per integral
+    const int* shard_of;            // [nprob] per-integral shard of nshards (mixed launches), or null: `shard`
     int nprob;
     int first_slot;                 // integral p -> slot first_slot + p
     double eps;
@@ -158,17 +165,15 @@ struct StreamParams {
     int shares;                     // jobs per integral: job j = share j % shares of integral j / shares
     unsigned epoch;                 // tags queue slots of this launch (ready[s] == epoch)
     unsigned qcap;                  // queue slots
-    unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+    unsigned long long stall_ticks; // s_memrealtime ticks (100 MHz) a waiting leader tolerates WITHOUT
+                                    // progress (queue head / tail / token count unchanged)
     Ctl* ctls;                      // per-slot control blocks; the queue uses ctls[first_slot]
-    WgPart* parts;                  // [slot * gridDim.x + wg]
-    double2* warea;                 // [slot * gridDim.x * NW + wave]: {hi, lo} area of that wave's leaves
+    unsigned long long* parts;      // [slot * gridDim.x + wg]: pack_cu(tasks, cu), per-CU launches only
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
     Chunk* chunks;
     Cellar* cellar;                 // [gridDim.x * NW]
     unsigned* ready;
     const ExpEntry* gtab;
-    double2* stk;                   // k_dfs: per-lane DFS stacks [wave][SDEPTH][64] {x, F(x)}
-    unsigned wstride;               // warea entries per slot (>= waves of any engine's grid)
     LaunchHint* hint;
     int per_cu;                     // also keep per-workgroup partials (per-CU task counts; lone integrals)
     int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
@@ -256,50 +261,35 @@ struct Acc {
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
 };
 
-// Add a wave's totals and double-double area to its integral's slot (lane 0). The area partial is
-// the wave's own (no other wave writes it); its first flush also lists the wave in the slot.
-__device__ __forceinline__ bool area_flush(double2* part, double hi, double lo) {
-    double* q = &part->x;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's previous flush has landed
-    double h0 = ld_wt(q), l0 = ld_wt(q + 1);
-    const bool first = h0 == 0.0 && l0 == 0.0;
-    dd_add_dd(h0, l0, hi, lo);
-    st_wt(q, h0);
-    st_wt(q + 1, l0);
-    return first;
-}
-__device__ __forceinline__ void slot_flush(Ctl& c, double2* part, unsigned t, unsigned l, unsigned m, double hi,
-                                           double lo, unsigned w) {
-    atomicAdd(&c.sums.tasks, (unsigned long long)t);
-    atomicAdd(&c.sums.leaves, (unsigned long long)l);
-    atomicMax(&c.sums.levels, m);
-    if (area_flush(part, hi, lo)) {   // (a partial that sums back to zero is listed twice: harmless, gathers dedupe)
-        const unsigned i = atomicAdd(&c.sums.ntouch, 1u);
-        if (i < TCAP) c.touch[i] = w;
-    }
-}
-
-// Flush a wave's accumulators for integral `tag` and reset them: the double-double area into the
-// wave's own partial (a plain read-modify-write: no other wave touches it); the counts into the slot
-// sums (device atomics, spread over the launch's integrals), or -- per-CU launches, where every wave
-// works on the same one or few integrals -- into the workgroup's LDS counts (fold_wg_counts at exit).
-// pc: the per-CU instance's LDS counts, [0,16) tasks, [16,32) accepted, [32,48) levels per integral.
-template <bool PCU>
-__device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, unsigned w_all,
-                                          WgState& S, unsigned long long* pc) {
-    double hi = 0.5 * a.hi, lo = 0.5 * a.lo;   // the wave accumulates doubled areas (exact halving)
+// Flush a wave's accumulators for integral `tag` and reset them: the wave's double-double area (hi
+// and lo, each exact) into the integral's exact accumulator; the counts into the slot sums (device
+// atomics, spread over the launch's integrals), or -- per-CU launches, where every wave works on the
+// same one or few integrals -- into the workgroup's LDS counts and LDS accumulator, folded into the
+// slot once per workgroup at exit (3072 waves would otherwise queue on one slot's lines).
+// pc: the per-CU instance's LDS counts, [0,16) tasks, [16,32) accepted, [32,48) levels per integral;
+// px: its LDS accumulators, one XSum per integral.
+template <int FID, bool PCU>
+__device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, WgState& S,
+                                          unsigned long long* pc, XSum* px) {
+    // the wave accumulates doubled areas for the built-in integrands (exact halving, aq_device.h)
+    double hi = area_scale<FID>() * a.hi, lo = area_scale<FID>() * a.lo;
     wave_sum_dd(hi, lo);
     const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
     if (lane == 0 && t) {
         atomicAdd(&S.tasks, (unsigned long long)t);
-        double2* part = &P.warea[(size_t)(P.first_slot + tag) * P.wstride + w_all];
         if constexpr (PCU) {
             atomicAdd(&pc[tag], (unsigned long long)t);
             atomicAdd(&pc[PCU_MAXK + tag], (unsigned long long)l);
             atomicMax(&pc[2 * PCU_MAXK + tag], (unsigned long long)m);
-            area_flush(part, hi, lo);   // the slot is marked for dense gathers at exit, not listed
+            xs_atomic_add(px[tag].limb, hi);
+            xs_atomic_add(px[tag].limb, lo);
         } else {
-            slot_flush(P.ctls[P.first_slot + tag], part, t, l, m, hi, lo, w_all);
+            Ctl& c = P.ctls[P.first_slot + tag];
+            atomicAdd(&c.sums.tasks, (unsigned long long)t);
+            atomicAdd(&c.sums.leaves, (unsigned long long)l);
+            atomicMax(&c.sums.levels, m);
+            xs_atomic_add(c.area.limb, hi);
+            xs_atomic_add(c.area.limb, lo);
         }
     }
     a.hi = a.lo = 0.0;
@@ -365,6 +355,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     __shared__ ExpEntry tab[128];
     __shared__ WgState S;
     __shared__ unsigned long long s_pc[PCU ? 3 * PCU_MAXK : 1];
+    __shared__ XSum s_px[PCU ? PCU_MAXK : 1];
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
 
     const unsigned tid = threadIdx.x;
@@ -382,16 +373,15 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         S.exited = 0; S.tasks = 0;
     }
     if (PCU && tid < 3u * PCU_MAXK) s_pc[tid] = 0ull;
+    if (PCU)
+        for (unsigned i = tid; i < (unsigned)(PCU_MAXK * XS_LIMBS); i += PT) s_px[i / XS_LIMBS].limb[i % XS_LIMBS] = 0;
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
-    if (PCU)
-        for (unsigned p = tid; p < (unsigned)P.nprob; p += blockDim.x)
-            P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid].cu = cu_slot();
     __syncthreads();   // the only workgroup barrier before the exit
 
     const double eps = P.eps;
-    const double eps2 = 2.0 * eps;   // the rounds compare doubled areas (task_step_k)
+    const double eps2 = doubled_areas<FID>() ? 2.0 * eps : eps;   // the rounds compare doubled areas (task_step_k)
     const int max_depth = P.max_depth;
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
     unsigned shares = (unsigned)P.shares;
@@ -445,7 +435,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     unsigned pf_n = 0;
     double pf_a = 0, pf_b = 0, pf_fa = 0, pf_fm = 0, pf_fb = 0;
     unsigned pf_dt = 0;
-    const unsigned long long t0 = rtc();
     unsigned long long cl0 = 0;
     if constexpr (DIAG) {
         if (tid == 0) s_dg[DG_T_START] = t_entry;
@@ -569,7 +558,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             if (k) {
                 if (ptag != tag) {     // the ring's new integral
-                    flush_acc<PCU>(P, acc, tag, lane, w_all, S, s_pc);
+                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
                     tag = ptag;
                 }
                 bot = 0;
@@ -583,9 +572,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 unsigned long long cs = 0;
                 if constexpr (DIAG) cs = clk();
                 const int p = (int)(job / shares);
-                const unsigned vw = (job % shares) * (unsigned)P.nshards + (unsigned)P.shard;
+                const unsigned shard_p = P.shard_of ? (unsigned)uni(P.shard_of[p]) : (unsigned)P.shard;
+                const unsigned vw = (job % shares) * (unsigned)P.nshards + shard_p;
                 if (p != tag) {
-                    flush_acc<PCU>(P, acc, tag, lane, w_all, S, s_pc);
+                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
                     tag = p;
                 }
                 // the bounds load goes out before the claim: waiting for it then leaves the claim (one
@@ -651,7 +641,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         acc.maxd = max(acc.maxd, d + 1u);
                         if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
                         if (d == dstar) {
-                            dd_add(acc.hi, acc.lo, 2.0 * leafarea);           // :199 -> :149 (doubled, exact)
+                            dd_add(acc.hi, acc.lo, leafarea / area_scale<FID>());   // :199 -> :149 (doubled, exact)
                             ++acc.leaves;
                             if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
                         } else if ((int)d + 1 >= max_depth) {
@@ -723,7 +713,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                                 acc.maxd = max(acc.maxd, d + 1u);
                                 if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
                                 if (d == dstar) {
-                                    dd_add(acc.hi, acc.lo, 2.0 * leafa[d * nb + kk]);   // :199 -> :149 (doubled)
+                                    dd_add(acc.hi, acc.lo, leafa[d * nb + kk] / area_scale<FID>());   // :199 -> :149 (doubled)
                                     ++acc.leaves;
                                     if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
                                 } else if ((int)d + 1 >= max_depth) {
@@ -791,13 +781,31 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     S.busy_token = 0;
                 }
                 const unsigned h = g_add(&qctl->q_head.v, 1u);
+                // the wait is bounded by time WITHOUT PROGRESS, not since launch: while work exists,
+                // busy waves donate to waiting tickets within POLL_ROUNDS rounds, and every donation
+                // or idle / busy transition moves the token count or the queue tail
+                unsigned long long t_prog = rtc();
+                int seen_tk = 0;
+                unsigned seen_tl = ~0u;
                 for (unsigned spins = 0;; ++spins) {
                     // both words are read every spin, issued together (one latency per spin)
                     const unsigned rv = h < P.qcap ? ld_wt(&P.ready[(size_t)h * READY_STRIDE]) : 0u;
                     const int tk = g_ld((int*)&qctl->q_tokens.v);
                     if (rv == P.epoch) { cmd = (int)h; break; }
                     if (tk == -(int)gridDim.x) { cmd = -1; break; }
-                    if ((spins & 63u) == 63u && rtc() - t0 > P.timeout_ticks) { err |= ERRB_TIMEOUT; cmd = -2; break; }
+                    if ((spins & 63u) == 63u) {
+                        const unsigned tl = g_ld(&qctl->q_tail.v);
+                        const unsigned long long now = rtc();
+                        if (tk != seen_tk || tl != seen_tl) {
+                            seen_tk = tk;
+                            seen_tl = tl;
+                            t_prog = now;
+                        } else if (now - t_prog > P.stall_ticks) {
+                            err |= ERRB_TIMEOUT;
+                            cmd = -2;
+                            break;
+                        }
+                    }
                     __builtin_amdgcn_s_sleep(2);
                 }
                 if (cmd >= 0) {
@@ -1050,9 +1058,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     }
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
-    flush_acc<PCU>(P, acc, tag, lane, w_all, S, s_pc);
+    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
     if (mixed) err |= ERRB_OVERFLOW;
     const unsigned werr = wave_or_u(err);
+    unsigned last_u = 0;
     if (lane == 0) {
         if (werr) {
             for (int p = 0; p < P.nprob; ++p)
@@ -1066,25 +1075,28 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
         // job-size hint for the next adaptive launch: the last wave of each workgroup adds the
         // workgroup's tasks, the last workgroup sets shares per integral for ~TASKS_PER_JOB per job
-        const bool last = (PCU || (P.adaptive & 2)) && atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u;
+        bool last = false;
+        if (PCU || (P.adaptive & 2)) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's LDS flushes precede its exit count
+            last = atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        last_u = last ? 1u : 0u;
         if (PCU && last) {
-            // per-CU launch: this workgroup's counts per integral, once -- its per-CU row (plain
-            // stores, one writer) and the slot sums (256 workgroups instead of every wave's flushes)
+            // per-CU launch: this workgroup's counts per integral, once -- its per-CU word (a plain
+            // store, one writer) and the slot sums (256 workgroups instead of every wave's flushes)
+            const unsigned cu = cu_slot();
             for (int p = 0; p < P.nprob; ++p) {
                 const unsigned long long t = __hip_atomic_load(&s_pc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned long long l = __hip_atomic_load(&s_pc[PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned m = (unsigned)__hip_atomic_load(&s_pc[2 * PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                WgPart* w = P.parts + (size_t)(P.first_slot + p) * gridDim.x + bid;
-                w->tasks = t;
-                w->leaves = l;
-                w->levels = m;
+                P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid] = pack_cu(t, cu);
                 Ctl& c = P.ctls[P.first_slot + p];
                 if (t) {
                     atomicAdd(&c.sums.tasks, t);
                     atomicAdd(&c.sums.leaves, l);
                     atomicMax(&c.sums.levels, m);
                 }
-                if (bid == 0) atomicMax(&c.sums.ntouch, TCAP + 1u);   // gathers / resets take the dense pass
             }
         }
         if (last && (P.adaptive & 2)) {
@@ -1099,6 +1111,20 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 __hip_atomic_store(&P.hint->shares_next, (unsigned)sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&P.hint->tasks, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&P.hint->exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if constexpr (PCU) {
+        // the workgroup's last wave folds the workgroup's exact area accumulators into the slots:
+        // one lane per limb, only the non-zero limbs (a handful per integral)
+        if (uni(__shfl(last_u, 0, 64))) {
+            for (int p = 0; p < P.nprob; ++p) {
+                long long* g = P.ctls[P.first_slot + p].area.limb;
+                for (unsigned i = lane; i < (unsigned)XS_LIMBS; i += 64) {
+                    const long long v = (long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(&s_px[p].limb[i]),
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&g[i]), (unsigned long long)v);
+                }
             }
         }
     }

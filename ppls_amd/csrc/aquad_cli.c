@@ -1,7 +1,7 @@
 /*
  * aquad_cli.c -- drop-in for `mpirun -n P ./aquadPartA` (/root/reference/aquadPartA.c main(), :78-123).
  *
- *   aquad [-n P] [--gpus G] [--eps E] [--a A] [--b B] [--f cosh4|sin_recip] [--per-cu] [--levels]
+ *   aquad [-n P] [--gpus G] [--eps E] [--a A] [--b B] [--f cosh4|sin_recip|user] [--per-cu] [--levels]
  *
  * Same observable surface as the reference: `Area=%lf`, a blank line, `Tasks Per Process`, the index
  * row and the count row (tab-terminated entries). Process 0 is the farmer and always reports 0 tasks
@@ -9,8 +9,8 @@
  * every GPU used, dealt round-robin (GPU-major, CU slot order) over the P-1 columns; P defaults to
  * 1 + G, i.e. one column per GPU. `--per-cu` prints one column per CU. P < 2 reproduces the
  * reference's error exactly (:86-90). Defaults are the reference's macros (:45-48).
- * With G > 1 the run is sharded: one host thread drives every GPU (aq_integrate_async on each, then
- * aq_fetch) and sums the per-GPU partial results.
+ * With G > 1 the run is sharded over an RCCL group (aq_group_create: one host thread drives every
+ * GPU; aq_integrate_group combines the shards with one grouped all-reduce / all-gather).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -21,11 +21,12 @@
 
 static void usage(void) {
     fprintf(stderr,
-            "usage: aquad [-n P] [--gpus G] [--eps E] [--a A] [--b B] [--f cosh4|sin_recip] [--per-cu] [--levels]\n");
+            "usage: aquad [-n P] [--gpus G] [--eps E] [--a A] [--b B] [--f cosh4|sin_recip|user] [--per-cu] "
+            "[--levels]\n");
 }
 
 int main(int argc, char **argv) {
-    aq_problem p = {AQ_F_COSH4, 0, 0.0, 5.0, 1e-3}; /* aquadPartA.c:45-48 */
+    aq_problem p = {AQ_F_COSH4, 0, 0.0, 5.0, 1e-3, 0, 0}; /* aquadPartA.c:45-48 */
     int nprocs = -1, gpus = 1, per_cu = 0, levels = 0;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
@@ -38,6 +39,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(a, "--f") && v) {
             if (!strcmp(v, "cosh4")) p.integrand = AQ_F_COSH4;
             else if (!strcmp(v, "sin_recip")) p.integrand = AQ_F_SIN_RECIP;
+            else if (!strcmp(v, "user")) p.integrand = AQ_F_USER;
             else { usage(); return 2; }
             ++i;
         } else if (!strcmp(a, "--per-cu")) per_cu = 1;
@@ -55,59 +57,54 @@ int main(int argc, char **argv) {
         return 1;
     }
     aq_ctx **ctx = calloc((size_t)gpus, sizeof(*ctx));
-    aq_result *part = calloc((size_t)gpus, sizeof(*part));
-    uint64_t *cu = calloc((size_t)gpus * AQ_CU_SLOTS, sizeof(uint64_t));
+    aq_group *grp = NULL;
     int rc = AQ_OK;
     for (int g = 0; g < gpus && rc == AQ_OK; ++g) rc = aq_ctx_create(g, &ctx[g]);
-    for (int g = 0; g < gpus && rc == AQ_OK; ++g) rc = aq_integrate_async(ctx[g], &p, g, gpus, 0);
-    for (int g = 0; g < gpus && rc == AQ_OK; ++g) {
-        rc = aq_fetch(ctx[g], 0, &part[g]);
-        if (rc == AQ_OK) aq_tasks_per_cu(ctx[g], cu + (size_t)g * AQ_CU_SLOTS, AQ_CU_SLOTS);
+    const int ncu = rc == AQ_OK ? aq_ctx_num_cus(ctx[0]) : 0;
+    uint64_t *per_gpu = calloc((size_t)gpus, sizeof(uint64_t));
+    uint64_t *cu = calloc((size_t)gpus * (size_t)(ncu > 0 ? ncu : 1), sizeof(uint64_t));
+    aq_result res;
+    memset(&res, 0, sizeof(res));
+    res.tasks_per_gpu = per_gpu;
+    res.tasks_per_cu = cu;
+    if (rc == AQ_OK) {
+        if (gpus == 1) {
+            rc = aq_integrate(ctx[0], &p, &res);
+        } else {
+            p.n_gpus = gpus;
+            rc = aq_group_create(ctx, gpus, &grp);
+            if (rc == AQ_OK) rc = aq_integrate_group(grp, &p, &res);
+        }
     }
     if (rc != AQ_OK) {
         fprintf(stderr, "aquad: %s\n", aq_strerror(rc));
         return 1;
     }
-    double area = 0.0;
-    uint64_t tasks = 0, accepted = 0;
-    uint32_t lv = 0;
-    int ncu = 0;
-    for (int g = 0; g < gpus; ++g) {
-        area += part[g].area;
-        tasks += part[g].tasks;
-        accepted += part[g].accepted;
-        if (part[g].levels > lv) lv = part[g].levels;
-        for (int s = 0; s < AQ_CU_SLOTS; ++s) ncu += cu[(size_t)g * AQ_CU_SLOTS + s] ? 1 : 0;
-    }
-    if (per_cu) nprocs = 1 + ncu;
-    uint64_t *tpp = calloc((size_t)nprocs, sizeof(uint64_t));
     if (!per_cu && nprocs - 1 == gpus) {
-        for (int g = 0; g < gpus; ++g) tpp[1 + g] = part[g].tasks;
+        aq_print_reference(stdout, &res);
     } else {
+        int cols = per_cu ? 0 : nprocs - 1;
+        if (per_cu)
+            for (int k = 0; k < gpus * ncu; ++k) cols += cu[k] ? 1 : 0;
+        uint64_t *tpp = calloc((size_t)cols + 1, sizeof(uint64_t));
         int k = 0;
-        for (int g = 0; g < gpus; ++g)
-            for (int s = 0; s < AQ_CU_SLOTS; ++s) {
-                uint64_t v = cu[(size_t)g * AQ_CU_SLOTS + s];
-                if (v) { tpp[1 + (k % (nprocs - 1))] += v; ++k; }
-            }
+        for (int c = 0; c < gpus * ncu; ++c)
+            if (cu[c]) { tpp[1 + (k % cols)] += cu[c]; ++k; }
+        aq_print_reference_procs(stdout, res.area, tpp, cols + 1);
+        free(tpp);
     }
-    aq_print_reference(stdout, area, tpp, nprocs);
     if (levels) {
         uint64_t t[AQ_MAX_LEVELS], l[AQ_MAX_LEVELS];
-        uint64_t ts[AQ_MAX_LEVELS] = {0}, ls[AQ_MAX_LEVELS] = {0};
-        for (int g = 0; g < gpus; ++g) {
-            aq_level_histogram(ctx[g], t, l, AQ_MAX_LEVELS);
-            for (int d = 0; d < AQ_MAX_LEVELS; ++d) { ts[d] += t[d]; ls[d] += l[d]; }
-        }
+        aq_level_histogram(ctx[0], t, l, AQ_MAX_LEVELS);
         fprintf(stdout, "\nLevel\tTasks\tAccepted\n");
-        for (uint32_t d = 0; d < lv; ++d)
-            fprintf(stdout, "%u\t%llu\t%llu\n", d, (unsigned long long)ts[d], (unsigned long long)ls[d]);
-        fprintf(stdout, "Total\t%llu\t%llu\n", (unsigned long long)tasks, (unsigned long long)accepted);
+        for (uint32_t d = 0; d < res.levels; ++d)
+            fprintf(stdout, "%u\t%llu\t%llu\n", d, (unsigned long long)t[d], (unsigned long long)l[d]);
+        fprintf(stdout, "Total\t%llu\t%llu\n", (unsigned long long)res.tasks, (unsigned long long)res.accepted);
     }
+    aq_group_destroy(grp);
     for (int g = 0; g < gpus; ++g) aq_ctx_destroy(ctx[g]);
-    free(tpp);
     free(cu);
-    free(part);
+    free(per_gpu);
     free(ctx);
     return 0;
 }

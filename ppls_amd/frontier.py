@@ -123,6 +123,9 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     fronts = [torch.empty((capacity, REC), dtype=torch.float64, device=dev) for _ in range(2)]
     nout = torch.zeros(1, dtype=torch.int32, device=dev)
     acc = torch.zeros(8, dtype=torch.float64, device=dev)
+    if dev.type == "cuda":
+        # the zeroing ran on torch's stream, the level steps run on the engine's own stream: order them
+        torch.cuda.synchronize(dev)
     cur = 0
     n = 0
     if rank == 0:
@@ -133,23 +136,35 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     max_front = 1
     per_level = []
     while True:
-        if depth >= max_depth + 1:
-            raise AquadError("frontier: maximum refinement depth reached")
         nxt = 1 - cur
-        stepper.step(integrand, fronts[cur], n, fronts[nxt], capacity, problem.eps, depth, max_depth, nout, acc)
-        stepper.sync()
-        produced = int(nout.item())
-        if produced > capacity:
-            raise AquadError(f"frontier capacity exceeded on rank {rank}: {produced} > {capacity}")
+        # a local failure is carried through the size exchange as a negative count, so every rank
+        # raises together instead of the others waiting in the collective (one all-gather per level)
+        err = ""
+        if depth >= max_depth + 1:
+            err = "maximum refinement depth reached"
+            produced = 0
+        else:
+            try:
+                stepper.step(integrand, fronts[cur], n, fronts[nxt], capacity, problem.eps, depth, max_depth, nout,
+                             acc)
+                stepper.sync()
+                produced = int(nout.item())
+            except AquadError as e:
+                err, produced = str(e), 0
+            if not err and produced > capacity:
+                err = f"capacity exceeded: {produced} > {capacity}"
         per_level.append(n)
-        cur, n, depth = nxt, produced, depth + 1
-        counts = torch.tensor([n], dtype=torch.int64, device=comm_dev)
-        if world > 1:
+        cur, n, depth = nxt, (0 if err else produced), depth + 1
+        counts = torch.tensor([-1 if err else n], dtype=torch.int64, device=comm_dev)
+        if distributed:
             gathered = [torch.zeros(1, dtype=torch.int64, device=comm_dev) for _ in range(world)]
             dist.all_gather(gathered, counts, group=group)
             sizes = [int(g.item()) for g in gathered]
         else:
-            sizes = [n]
+            sizes = [int(counts.item())]
+        failed = [r for r, v in enumerate(sizes) if v < 0]
+        if failed:
+            raise AquadError(f"frontier: rank {failed[0]} failed" + (f" ({err})" if err else ""))
         total = sum(sizes)
         max_front = max(max_front, total)
         if total == 0:
@@ -171,7 +186,7 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
                         ops.append(dist.P2POp(dist.isend, buf, dst, group))
                         send_end -= k
                     elif dst == rank:
-                        if recv_at + k > capacity:
+                        if recv_at + k > capacity:   # every rank computes the same plan: all raise together
                             raise AquadError(f"frontier capacity exceeded on rank {rank} while receiving")
                         buf = fronts[cur][recv_at:recv_at + k]
                         if buf.device != comm_dev:
@@ -190,7 +205,7 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
                 n = send_end + (recv_at - n)      # a rank only sends or only receives
     stepper.sync()
     mine = acc.to(comm_dev)
-    if world > 1:
+    if distributed:
         accs = [torch.zeros(8, dtype=torch.float64, device=comm_dev) for _ in range(world)]
         dist.all_gather(accs, mine, group=group)
         lv = torch.tensor(per_level, dtype=torch.int64, device=comm_dev)

@@ -28,6 +28,18 @@ def batch_golden():
 
 
 @pytest.fixture(scope="session")
+def deep_golden():
+    with open(os.path.join(GOLDEN, "deep.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def plugin_bits():
+    z = np.load(os.path.join(GOLDEN, "plugin_bits.npz"))  # allow_pickle=False (default)
+    return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
 def libm_bits():
     z = np.load(os.path.join(GOLDEN, "libm_bits.npz"))  # allow_pickle=False (default)
     return {k: z[k] for k in z.files}
@@ -38,3 +50,23 @@ def oracle():
     from oracle import pyoracle
     pyoracle.lib()
     return pyoracle
+
+
+def exact_row(values, tasks=0, accepted=0, spilled=0, levels=0, error=0):
+    """An exact row (include/aquad.h AQ_EXACT_ROW) of the given doubles, built with Python integers:
+    limbs whose weighted sum is exactly sum(values) (the CPU shard backends of the dist tests)."""
+    import math
+    X = 0
+    for v in values:
+        if v == 0.0:
+            continue
+        m, e = math.frexp(v)
+        X += int(m * 2 ** 53) << (e - 53 + 1088)
+    row = np.zeros(72, np.int64)
+    for i in range(67):
+        row[i] = X & 0xffffffff
+        X >>= 32
+    row[67] = X
+    row[68], row[69], row[70] = tasks, accepted, spilled
+    row[71] = levels | (error << 32)
+    return row

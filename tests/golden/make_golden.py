@@ -15,6 +15,8 @@ Outputs (data only, no code of the reference):
   trees.json      per config: counts, per-level histograms, areas, reference stdout
   libm_bits.npz   x, cosh(x), exp(x) as uint64 bit patterns from the host libm
   batch.json      splitmix64 batch bounds KATs and per-integral counts (config C3 prefix)
+  plugin_bits.npz x, F(x) of the AQ_F_USER plug-in (exp(-x*x), host libm) as uint64 bit patterns
+  deep.json       eps 1e-14 .. 1e-16 cosh4 trees pinned by the reference binary's task totals
 """
 import json
 import os
@@ -162,10 +164,79 @@ def batch():
           float(l10.mean()))
 
 
+PLUGIN_CONFIGS = [
+    # the AQ_F_USER plug-in (ppls_amd/csrc/plugins/aq_user_gauss.h): the reference binary with line 46
+    # replaced by `#define F(arg) exp(-(arg)*(arg))` (oracle/Makefile), A = 0, B = 5 unchanged
+    ("gauss_eps1e-10", 1e-10, "aquadPartA_gauss_eps1e-10"),
+    ("gauss_eps1e-13", 1e-13, "aquadPartA_gauss_eps1e-13"),
+]
+
+
+def plugin():
+    """Add the plug-in integrand's trees to trees.json (pinned by the reference binary built with
+    that F) and its F bit patterns (host libm exp) to plugin_bits.npz."""
+    path = os.path.join(OUT, "trees.json")
+    with open(path) as f:
+        out = json.load(f)
+    for name, eps, ref in PLUGIN_CONFIGS:
+        r = O.integrate(O.USER, 0.0, 5.0, eps)
+        rec = {"integrand": "gauss", "a": 0.0, "b": 5.0, "eps": eps, "tasks": r.tasks, "leaves": r.leaves,
+               "levels": r.levels, "tasks_per_level": r.tasks_per_level, "leaves_per_level": r.leaves_per_level,
+               "area_quad": r.area_quad_str, "area_lifo_hex": float(r.area_lifo).hex(),
+               "area_lifo_printed": "%f" % r.area_lifo}
+        refrun = run_reference(ref, 5)
+        assert refrun["tasks_total"] == r.tasks, (name, refrun["tasks_total"], r.tasks)
+        assert refrun["area_printed"] == "%f" % (r.area_quad_hi + r.area_quad_lo), (name, refrun["area_printed"])
+        ref2 = run_reference(ref, 2)
+        assert ref2["tasks_total"] == r.tasks
+        assert ref2["area_printed"] == "%f" % r.area_lifo
+        rec["reference"] = refrun
+        rec["reference_p2"] = ref2
+        out[name] = rec
+        print(name, r.tasks, r.leaves, r.levels, r.area_quad_str)
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    rng = np.random.default_rng(20261016)
+    x = np.concatenate([[0.0, -0.0, 2.0 ** -28, 2.0 ** -27.5, 1.0, 5.0, 22.0, 22.7, 26.0, 27.2, 27.3, 28.0, 40.0],
+                        rng.uniform(-5.0, 5.0, 4000), rng.uniform(22.0, 27.5, 1000), rng.uniform(-1e-8, 1e-8, 200)])
+    F = O.F(x, O.USER, O.HOST_LIBM)
+    assert (O.F(x, O.USER).view(np.uint64) == F.view(np.uint64)).all()
+    np.savez_compressed(os.path.join(OUT, "plugin_bits.npz"), x=x.view(np.uint64), F=F.view(np.uint64))
+
+
+DEEP_EPS = (("1e-14", 1e-14), ("1e-15", 1e-15), ("1e-16", 1e-16))
+
+
+def deep():
+    """Deep cosh4 trees (eps 1e-14 .. 1e-16, 31 M .. 150 M tasks) pinned by the reference binary
+    itself (mpirun -n 5, ~15-80 s each here): its printed task total and Area= line are recorded and
+    the oracle's restatement must reproduce both. The oracle adds the accepted count, depth and the
+    quad-precision area. Output: deep.json."""
+    out = {}
+    for tag, eps in DEEP_EPS:
+        refrun = run_reference("aquadPartA_eps" + tag, 5)
+        r = O.integrate(O.COSH4, 0.0, 5.0, eps, maxlev=128)
+        assert refrun["tasks_total"] == r.tasks, (tag, refrun["tasks_total"], r.tasks)
+        # the reference's own arrival-order sum (:149) drifts from the exact sum by up to ~1e-13
+        # relative at these sizes (SURVEY H6), which can move its 6th printed decimal: compare within
+        # the print rounding plus the north star's 1e-12 relative tolerance
+        exact = r.area_quad_hi + r.area_quad_lo
+        assert abs(float(refrun["area_printed"]) - exact) <= 5e-7 + 1e-12 * exact, (tag, refrun["area_printed"])
+        out["cosh4_eps" + tag] = {
+            "integrand": "cosh4", "a": 0.0, "b": 5.0, "eps": eps,
+            "tasks": r.tasks, "leaves": r.leaves, "levels": r.levels,
+            "tasks_per_level": r.tasks_per_level, "leaves_per_level": r.leaves_per_level,
+            "area_quad": r.area_quad_str, "reference": refrun,
+        }
+        print("deep", tag, r.tasks, r.leaves, r.levels, refrun["area_printed"])
+    with open(os.path.join(OUT, "deep.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     if not shutil.which(MPIRUN) and not os.path.exists(MPIRUN):
         print("warning: no mpirun; reference stdout will not be recorded")
     O.build()
-    trees()
-    libm_bits()
-    batch()
+    which = sys.argv[1:] or ["trees", "plugin", "libm_bits", "batch", "deep"]
+    for name in which:
+        {"trees": trees, "plugin": plugin, "libm_bits": libm_bits, "batch": batch, "deep": deep}[name]()

@@ -85,3 +85,46 @@ def test_group_tasks_deals_cus_round_robin():
     from ppls_amd.aquad import group_tasks
     assert group_tasks({5: 1, 1: 10, 9: 100}, 2) == [10 + 100, 1]
     assert sum(group_tasks({i: i for i in range(256)}, 4)) == sum(range(256))
+
+
+def test_print_reference_from_result(lib, tmp_path, trees):
+    """aq_print_reference(FILE*, const aq_result*) -- main()'s printout (aquadPartA.c:107-117) from a
+    result struct: farmer 0, then one column per GPU (tasks_per_gpu)."""
+    import ctypes
+    import numpy as np
+    from ppls_amd import _lib, format_reference
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    per_gpu = np.array([1679, 1605, 1682, 1601], np.uint64)   # the header's sample split (:34-36)
+    r = _lib.aq_result()
+    r.area = 7583461.801486495
+    r.tasks = int(per_gpu.sum())
+    r.n_gpus = 4
+    r.tasks_per_gpu = per_gpu.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    path = tmp_path / "out.txt"
+    f = libc.fopen(str(path).encode(), b"w")
+    lib.aq_print_reference(f, ctypes.byref(r))
+    lib.aq_print_reference_procs(f, 7583461.801486495, (ctypes.c_uint64 * 2)(0, 6567), 2)
+    libc.fclose(f)
+    text = path.read_text()
+    want = format_reference(r.area, [0] + [int(v) for v in per_gpu])
+    assert text.startswith(want)
+    assert text[len(want):] == format_reference(r.area, [0, 6567])
+    assert want.splitlines()[0] == "Area=7583461.801486"
+
+
+def test_exact_round_is_exported_host_code(lib):
+    """aq_exact_round runs on the host (no GPU): limbs of 1.5 * 2^0 round to 1.5."""
+    import ctypes
+    import numpy as np
+    limbs = np.zeros(68, np.int64)
+    # 1.5 = 3 * 2^-1 -> bit position -1 + 1088 = 1087 -> limb 33, bit 31
+    limbs[33] = 3 << 31 & 0xffffffff
+    limbs[34] = (3 << 31) >> 32
+    assert lib.aq_exact_round(limbs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))) == 1.5
+
+
+def test_user_integrand_name(lib):
+    assert lib.aq_user_integrand_name().startswith(b"gauss")

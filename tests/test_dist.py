@@ -2,13 +2,18 @@
 
 The shard backend is the CPU oracle's restatement of the device partition (oracle/aq_oracle.c
 aqo_integrate_shard), so the collective path is exercised exactly as it runs over RCCL, and the
-combined result must equal the single-process tree bit for bit in counts."""
+combined result must equal the single-process tree bit for bit in counts. Also: a failing rank makes
+every rank raise (no hang), and the rebalanced batch keeps exact counts and balances the load."""
 import os
 import socket
+import sys
 
+import numpy as np
 import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -19,48 +24,132 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _init(rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    for p in (ROOT, os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _shard_row(p, r, w):
+    from conftest import exact_row
+    from oracle import pyoracle as O
+    o = O.integrate_shard(r, w, G=256, integrand=p.integrand, a=p.a, b=p.b, eps=p.eps)
+    return exact_row([o.area_quad_hi, o.area_quad_lo], o.tasks, o.leaves, 0, o.levels)
+
+
+def _worker(rank, world, port, q):
+    _init(rank, world, port)
     try:
-        import sys
-        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        sys.path.insert(0, root)
-        from oracle import pyoracle as O
-        from ppls_amd.aquad import Problem, Result
+        from ppls_amd.aquad import Problem
         from ppls_amd.dist import integrate_distributed, tasks_per_process
-
-        def shard_fn(p, r, w):
-            o = O.integrate_shard(r, w, G=256, integrand=p.integrand, a=p.a, b=p.b, eps=p.eps)
-            return Result(o.area, o.tasks, o.leaves, o.levels, 256)
-
         out = []
-        for prob in (Problem(eps=1e-8), Problem(integrand=1, a=1e-4, b=1.0, eps=1e-7)):
-            res = integrate_distributed(prob, shard_fn=shard_fn)
+        for prob in (Problem(eps=1e-8), Problem(integrand=1, a=1e-4, b=1.0, eps=1e-7), Problem(integrand=2, eps=1e-11)):
+            res = integrate_distributed(prob, shard_fn=_shard_row)
             out.append((res.area, res.tasks, res.accepted, res.levels, tasks_per_process(res)))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_sharded_combine_equals_single(world, oracle):
+def _run(target, world, *args, timeout=300):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=300) for _ in range(world))
+    results = dict(q.get(timeout=timeout) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = [oracle.integrate(eps=1e-8), oracle.integrate(oracle.SIN_RECIP, 1e-4, 1.0, 1e-7)]
+    return results
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_combine_equals_single(world, oracle):
+    results = _run(_worker, world)
+    ref = [oracle.integrate(eps=1e-8), oracle.integrate(oracle.SIN_RECIP, 1e-4, 1.0, 1e-7),
+           oracle.integrate(oracle.USER, 0.0, 5.0, 1e-11)]
     for rank in range(world):
         for got, want in zip(results[rank], ref):
             area, tasks, acc, levels, tpp = got
             assert tasks == want.tasks and acc == want.leaves and levels == want.levels
             assert abs(area - want.area) <= 1e-12 * abs(want.area)
             assert tpp[0] == 0 and sum(tpp) == want.tasks and len(tpp) == world + 1
-    assert results[0] == results[1]
+    assert all(results[r] == results[0] for r in range(world))   # identical on every rank
+
+
+def _fail_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        from ppls_amd.aquad import AquadError, Problem
+        from ppls_amd.dist import integrate_distributed
+
+        def shard_fn(p, r, w):
+            if r == 1:
+                raise AquadError("injected: maximum refinement depth reached", -5)
+            return _shard_row(p, r, w)
+        try:
+            integrate_distributed(Problem(eps=1e-6), shard_fn=shard_fn)
+            q.put((rank, "no error"))
+        except AquadError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_failing_rank_raises_everywhere():
+    """a rank that fails before the collective must not leave the others hanging."""
+    results = _run(_fail_worker, 2, timeout=120)
+    assert all("rank 1 failed" in results[r] and "depth" in results[r] for r in range(2)), results
+
+
+class _OracleBatchRunner:
+    """CPU stand-in for HipBatchRunner: each unit (integral, shard s of S) through the oracle's shard
+    restatement (any partition shared by all ranks sums to the whole tree)."""
+
+    def run(self, a, b, shards, nshards, eps, integrand):
+        from conftest import exact_row
+        from oracle import pyoracle as O
+        rows = []
+        for x, y, s in zip(a, b, shards):
+            o = O.integrate_shard(int(s), int(nshards), G=2, integrand=integrand, a=float(x), b=float(y), eps=eps)
+            rows.append(exact_row([o.area_quad_hi, o.area_quad_lo], o.tasks, o.leaves, 0, o.levels))
+        self.ms = 0.0
+        return np.array(rows, np.int64).reshape(-1, 72)
+
+
+def _batch_worker(rank, world, port, rebalance, q):
+    _init(rank, world, port)
+    try:
+        from ppls_amd.dist import integrate_batch_distributed
+        n = 12
+        a = np.full(n, 1e-4)
+        b = np.ones(n)
+        r = integrate_batch_distributed(a, b, 1e-7, integrand=1, runner=_OracleBatchRunner(),
+                                        shards_per_integral=4 * world, window=3, rebalance=rebalance)
+        q.put((rank, (r.area.tolist(), r.tasks.tolist(), r.accepted.tolist(), r.tasks_per_rank, r.rounds)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("rebalance", [False, True])
+def test_gloo_rebalanced_batch(oracle, rebalance):
+    """sin(1/x) batch over 2 ranks: exact per-integral counts either way; with rebalancing the ranks'
+    task counts end within 15 % of each other, where the static shard split leaves them ~1.5x apart."""
+    world = 2
+    results = _run(_batch_worker, world, rebalance, timeout=300)
+    want = oracle.integrate(oracle.SIN_RECIP, 1e-4, 1.0, 1e-7)
+    area, tasks, acc, per_rank, rounds = results[0]
+    assert all(t == want.tasks for t in tasks) and all(x == want.leaves for x in acc)
+    assert all(abs(v - want.area) <= 1e-12 * abs(want.area) for v in area)
+    assert sum(per_rank) == 12 * want.tasks and rounds == (5 if rebalance else 4)   # a short first round
+    ratio = max(per_rank) / min(per_rank)
+    if rebalance:
+        assert ratio < 1.15, per_rank
+    else:
+        assert ratio > 1.3, per_rank
+    assert results[1] == results[0]

@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 AREA_RTOL = 1e-12  # BASELINE.json north_star: "its area to a stated relative tolerance of 1e-12"
 
 TREE_CASES = ["cosh4_eps1e-3", "cosh4_eps1e-6", "cosh4_eps1e-8", "cosh4_eps1e-10", "cosh4_eps1e-12",
-              "sin_recip_eps1e-9", "cosh4_eps1e3_root_leaf", "cosh4_empty_interval", "cosh4_neg_domain"]
+              "sin_recip_eps1e-9", "cosh4_eps1e3_root_leaf", "cosh4_empty_interval", "cosh4_neg_domain",
+              "gauss_eps1e-10", "gauss_eps1e-13"]
 
 
 @pytest.fixture(scope="module")
@@ -25,9 +26,12 @@ def ctx():
     c.close()
 
 
+FIDS = {"cosh4": 0, "sin_recip": 1, "gauss": 2}
+
+
 def _problem(g):
     from ppls_amd import Problem
-    return Problem(0 if g["integrand"] == "cosh4" else 1, g["a"], g["b"], g["eps"])
+    return Problem(FIDS[g["integrand"]], g["a"], g["b"], g["eps"])
 
 
 def _area_ok(got, quad_str):
@@ -85,7 +89,7 @@ def test_persistent_tree_parity(ctx, trees, name):
     assert r.tasks_per_level == g["tasks_per_level"]
     assert r.leaves_per_level == g["leaves_per_level"]
     assert _area_ok(r.area, g["area_quad"]), (r.area, g["area_quad"])
-    if g["integrand"] == "cosh4":   # F bit-exact (sin(1/x) is faithful only): leaf areas are the
+    if g["integrand"] != "sin_recip":   # F bit-exact (sin(1/x) is faithful only): leaf areas are the
         # reference's; lanes sum their own few leaves in double, everything above is double-double,
         # so the area is within 1 ulp of the correctly rounded sum of the leaf areas
         want = float(g["area_quad"])
@@ -95,7 +99,8 @@ def test_persistent_tree_parity(ctx, trees, name):
 
 
 @pytest.mark.parametrize("name", ["cosh4_eps1e-3", "cosh4_eps1e-8", "cosh4_eps1e-10", "sin_recip_eps1e-9",
-                                  "cosh4_eps1e3_root_leaf", "cosh4_empty_interval", "cosh4_neg_domain"])
+                                  "cosh4_eps1e3_root_leaf", "cosh4_empty_interval", "cosh4_neg_domain",
+                                  "gauss_eps1e-13"])
 def test_level_path_parity(ctx, trees, name):
     g = trees[name]
     r = ctx.integrate_levels(_problem(g))
@@ -117,7 +122,7 @@ def test_reference_known_answer_printout(ctx, trees):
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 8])
-@pytest.mark.parametrize("name", ["cosh4_eps1e-10", "sin_recip_eps1e-9"])
+@pytest.mark.parametrize("name", ["cosh4_eps1e-10", "cosh4_eps1e-12", "sin_recip_eps1e-9", "gauss_eps1e-13"])
 def test_shards_match_oracle_partition(ctx, trees, oracle, name, nshards):
     g = trees[name]
     p = _problem(g)
@@ -204,20 +209,17 @@ def test_many_integrals_one_launch(ctx, oracle, trees):
         assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
 
 
-@pytest.mark.parametrize("engine", ["stream", "dfs"])
-def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden, engine):
+def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
     """MAXK integrals with random bounds in ONE persistent launch (the bench's launch shape); the
     first 256 against the committed golden fixture, all of them against the oracle."""
     k = ctx.max_integrals_per_launch
     a, b = oracle.batch_bounds(k)
     ctx.set_level_histograms(False)
-    ctx.set_engine(engine)
     try:
         ctx.integrate_many_async(a, b, 1e-3, first_slot=0)
         got = [ctx.fetch(i) for i in range(k)]
     finally:
         ctx.set_level_histograms(True)
-        ctx.set_engine("auto")
     assert [g.accepted for g in got[:256]] == batch_golden["leaves_eps1e-3_first256"]
     want = [float.fromhex(h) for h in batch_golden["area_eps1e-3_first256_hex"]]
     assert all(abs(g.area - w) <= AREA_RTOL * abs(w) for g, w in zip(got, want))
@@ -247,7 +249,6 @@ def test_large_jobs_and_cellar(trees, monkeypatch):
     monkeypatch.setenv("AQ_GSPLIT", "8")
     c = Context(0)
     try:
-        c.set_engine("stream")
         c.set_level_histograms(False)
         c.set_diagnostics(True)
         g = trees["cosh4_eps1e-12"]
@@ -290,38 +291,33 @@ def test_back_to_back_launches_same_slots(ctx, oracle, batch_golden, trees):
     assert (o[:, :, 3] == 0).all()
 
 
-@pytest.mark.parametrize("engine", ["stream", "dfs"])
-def test_engine_parity(ctx, oracle, trees, engine):
-    """Both persistent engines, forced: lone integrals (every golden tree), a 40-integral launch of
-    mixed bounds, and a sharded launch -- counts bit-exact, areas within 1e-12."""
-    ctx.set_engine(engine)
-    try:
-        for name in ["cosh4_eps1e-3", "cosh4_eps1e-10", "cosh4_eps1e-12", "sin_recip_eps1e-9", "cosh4_empty_interval"]:
-            g = trees[name]
-            r = ctx.integrate(_problem(g))
-            assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"]), (engine, name)
-            assert r.tasks_per_level == g["tasks_per_level"]
-            assert _area_ok(r.area, g["area_quad"])
-        a, b = oracle.batch_bounds(32)
-        a = np.concatenate([a, np.zeros(8)])
-        b = np.concatenate([b, np.full(8, 5.0)])
-        ctx.integrate_many_async(a, b, 1e-8, first_slot=100)
-        oa, ot, ol = oracle.integrate_batch(a, b, 1e-8)
-        for i in range(a.size):
-            r = ctx.fetch(100 + i, detail=True)
-            assert (r.tasks, r.accepted) == (int(ot[i]), int(ol[i])), (engine, i)
-            assert abs(r.area - oa[i]) <= AREA_RTOL * abs(oa[i])
-        g = trees["cosh4_eps1e-10"]
-        tot = [0, 0]
-        for s in range(5):   # 5 shards: the seeding's many-node path on both engines' grids
-            r = ctx.integrate_shard(_problem(g), s, 5)
-            o = oracle.integrate_shard(s, 5, G=ctx.num_workers, S=2, integrand=0, a=0.0, b=5.0, eps=1e-10)
-            assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
-            tot[0] += r.tasks
-            tot[1] += r.accepted
-        assert tot == [g["tasks"], g["leaves"]]
-    finally:
-        ctx.set_engine("auto")
+def test_mixed_bounds_and_shards(ctx, oracle, trees):
+    """Lone integrals of every golden tree, a 40-integral launch of mixed bounds, and a 5-way sharded
+    integral (the seeding's many-node path) -- counts bit-exact, areas within 1e-12."""
+    for name in ["cosh4_eps1e-3", "cosh4_eps1e-10", "cosh4_eps1e-12", "sin_recip_eps1e-9", "cosh4_empty_interval"]:
+        g = trees[name]
+        r = ctx.integrate(_problem(g))
+        assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"]), name
+        assert r.tasks_per_level == g["tasks_per_level"]
+        assert _area_ok(r.area, g["area_quad"])
+    a, b = oracle.batch_bounds(32)
+    a = np.concatenate([a, np.zeros(8)])
+    b = np.concatenate([b, np.full(8, 5.0)])
+    ctx.integrate_many_async(a, b, 1e-8, first_slot=100)
+    oa, ot, ol = oracle.integrate_batch(a, b, 1e-8)
+    for i in range(a.size):
+        r = ctx.fetch(100 + i, detail=True)
+        assert (r.tasks, r.accepted) == (int(ot[i]), int(ol[i])), i
+        assert abs(r.area - oa[i]) <= AREA_RTOL * abs(oa[i])
+    g = trees["cosh4_eps1e-10"]
+    tot = [0, 0]
+    for s in range(5):
+        r = ctx.integrate_shard(_problem(g), s, 5)
+        o = oracle.integrate_shard(s, 5, G=ctx.num_workers, S=2, integrand=0, a=0.0, b=5.0, eps=1e-10)
+        assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
+        tot[0] += r.tasks
+        tot[1] += r.accepted
+    assert tot == [g["tasks"], g["leaves"]]
 
 
 def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
@@ -353,25 +349,25 @@ def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
         ctx.set_level_histograms(True)
 
 
-# Deeper trees than the committed fixtures (counts of the reference's
-# arithmetic): up to 150 M tasks and depth 31 in one launch, alone and as a small batch.
-DEEP = {1e-14: (30870291, 15435146), 1e-15: (66989173, 33494587), 1e-16: (150257851, 75128926)}
-
-
-@pytest.mark.parametrize("eps", sorted(DEEP))
-def test_deep_trees(ctx, oracle, eps):
+# Deep trees (up to 150 M tasks, depth 31, in one launch), pinned by the reference binary's own task
+# totals (tests/golden/deep.json, make_golden.py deep): alone and as a small batch.
+@pytest.mark.parametrize("name", ["cosh4_eps1e-14", "cosh4_eps1e-15", "cosh4_eps1e-16"])
+def test_deep_trees(ctx, deep_golden, name):
     from ppls_amd import Problem
+    g = deep_golden[name]
+    assert g["reference"]["tasks_total"] == g["tasks"]
+    ctx.set_level_histograms(True)
+    r = ctx.integrate(Problem(eps=g["eps"]))
+    assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"])
+    assert r.tasks_per_level == g["tasks_per_level"] and r.leaves_per_level == g["leaves_per_level"]
+    assert abs(r.area - float(g["area_quad"])) <= math.ulp(float(g["area_quad"]))
+    assert sum(r.tasks_per_cu.values()) == r.tasks
     ctx.set_level_histograms(False)
     try:
-        r = ctx.integrate(Problem(eps=eps))
-        assert (r.tasks, r.accepted) == DEEP[eps]
-        assert sum(r.tasks_per_cu.values()) == r.tasks
-        ctx.integrate_many_async(np.zeros(4), np.full(4, 5.0), eps, first_slot=0)
+        ctx.integrate_many_async(np.zeros(4), np.full(4, 5.0), g["eps"], first_slot=0)
         got = [ctx.fetch(i) for i in range(4)]
-        assert all((g.tasks, g.accepted) == DEEP[eps] for g in got)
-        if eps == 1e-14:
-            o = oracle.integrate(eps=eps)
-            assert all(abs(g.area - o.area) <= AREA_RTOL * o.area for g in got + [r])
+        assert all((x.tasks, x.accepted) == (g["tasks"], g["leaves"]) for x in got)
+        assert all(_area_ok(x.area, g["area_quad"]) for x in got)
     finally:
         ctx.set_level_histograms(True)
 
@@ -386,3 +382,144 @@ def test_sin_recip_deeper(ctx, oracle, eps):
     assert (r.tasks, r.accepted, r.levels) == (o.tasks, o.leaves, o.levels)
     assert r.tasks_per_level == o.tasks_per_level
     assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
+
+
+def test_c3_eps1e10_max_launch(ctx, oracle, batch_golden):
+    """SURVEY config 3 at its throughput tolerance in ONE launch of the maximum size (65536 random
+    bounds, splitmix64): the first 200 against the fixture the oracle committed (tests/golden/
+    batch.json), 48 more drawn across the launch against the oracle live, every integral T = 2L - 1,
+    and a second launch of the same integrals in reverse order (another schedule) agreeing."""
+    k = ctx.max_integrals_per_launch
+    a, b = oracle.batch_bounds(k)
+    ctx.set_level_histograms(False)
+    try:
+        ctx.integrate_many_async(a, b, 1e-10, first_slot=0)
+        ctx.synchronize()
+        rows = [ctx.fetch(i) for i in range(k)]
+        ctx.integrate_many_async(a[::-1].copy(), b[::-1].copy(), 1e-10, first_slot=0)
+        rev = [ctx.fetch(k - 1 - i) for i in range(k)]
+    finally:
+        ctx.set_level_histograms(True)
+    n10 = batch_golden["n_eps1e-10"]
+    assert [r.accepted for r in rows[:n10]] == batch_golden["leaves_eps1e-10"]
+    want = [float.fromhex(h) for h in batch_golden["area_eps1e-10_hex"]]
+    assert all(abs(r.area - w) <= math.ulp(w) for r, w in zip(rows, want))
+    assert all(r.tasks == 2 * r.accepted - 1 for r in rows)
+    assert [(r.tasks, r.accepted) for r in rev] == [(r.tasks, r.accepted) for r in rows]
+    assert all(abs(x.area - y.area) <= 2 * math.ulp(y.area) for x, y in zip(rev, rows))
+    pick = np.random.default_rng(7).choice(np.arange(n10, k), 48, replace=False)
+    oa, ot, ol = oracle.integrate_batch(a[pick], b[pick], 1e-10)
+    for j, i in enumerate(pick):
+        assert (rows[i].tasks, rows[i].accepted) == (int(ot[j]), int(ol[j])), i
+        assert abs(rows[i].area - oa[j]) <= AREA_RTOL * abs(oa[j])
+
+
+def test_stall_bound_is_not_a_run_time_cap(ctx, deep_golden):
+    """A launch far longer than the stall bound (50 ms here; 32 integrals at eps=1e-14, ~1e9 tasks)
+    completes with exact counts: the on-device wait is bounded by time without progress only."""
+    g = deep_golden["cosh4_eps1e-14"]
+    ctx.set_level_histograms(False)
+    ctx.set_stall_timeout(50.0)
+    try:
+        ctx.kernel_timing(True)
+        ctx.integrate_many_async(np.zeros(32), np.full(32, 5.0), 1e-14, first_slot=0)
+        ms, n = ctx.kernel_time()
+        ctx.kernel_timing(False)
+        got = [ctx.fetch(i) for i in range(32)]
+    finally:
+        ctx.set_stall_timeout(10000.0)
+        ctx.set_level_histograms(True)
+    assert ms > 200.0   # the launch really outlived the bound several times over
+    assert all((x.tasks, x.accepted) == (g["tasks"], g["leaves"]) for x in got)
+
+
+def test_plugin_integrand_bit_exact(ctx, plugin_bits):
+    """AQ_F_USER (the default plug-in, exp(-x*x)) on the device equals the host libm bit for bit,
+    including exp's tiny-argument and subnormal-result paths."""
+    from ppls_amd import USER, user_integrand_name
+    assert user_integrand_name().startswith("gauss")
+    x = plugin_bits["x"].view(np.float64)
+    got = ctx.eval_integrand(x, integrand=USER).view(np.uint64)
+    bad = np.nonzero(got != plugin_bits["F"])[0]
+    assert bad.size == 0, [(float(x[i]), hex(int(got[i])), hex(int(plugin_bits["F"][i]))) for i in bad[:8]]
+
+
+def test_plugin_reference_printout(ctx, trees):
+    """The plug-in tree against the reference binary built with that F (its printed Area= and task total)."""
+    for name in ["gauss_eps1e-10", "gauss_eps1e-13"]:
+        g = trees[name]
+        r = ctx.integrate(_problem(g))
+        assert r.tasks == g["reference"]["tasks_total"]
+        assert "%f" % r.area == g["reference"]["area_printed"]
+
+
+def test_context_footprint(ctx):
+    """No per-wave area partials or second engine: a context holds well under 2 GiB (round 1: ~7 GiB)."""
+    assert ctx.device_bytes < 2 * 2 ** 30, ctx.device_bytes
+
+
+def test_exact_rows_sum_over_shards(ctx, trees):
+    """Exact rows (int64 limbs) summed over the shards of a partition round to the whole area within
+    one ulp of the correctly rounded leaf sum, and the counts add up."""
+    from ppls_amd import Problem, exact_round
+    g = trees["cosh4_eps1e-12"]
+    tot = np.zeros(72, np.int64)
+    for s in range(8):
+        ctx.integrate_async(Problem(eps=1e-12), slot=s, shard=s, nshards=8)
+    ctx.synchronize()
+    for s in range(8):
+        row = ctx.fetch_exact(s)
+        assert row[71] >> 32 == 0   # no error bits
+        tot[:71] += row[:71]
+    assert (int(tot[68]), int(tot[69])) == (g["tasks"], g["leaves"])
+    want = float(g["area_quad"])
+    assert abs(exact_round(tot) - want) <= math.ulp(want)
+
+
+def test_mixed_shard_launch(ctx, oracle, trees):
+    """One launch holding different shards of different integrals (the rebalanced batch's launch
+    shape): every entry equals the oracle's shard, and each integral's shards sum to its tree."""
+    g = trees["sin_recip_eps1e-9"]
+    N = 8
+    shards = np.array([s for s in range(N) for _ in range(3)], np.int32)[::-1].copy()
+    a = np.full(shards.size, 1e-4)
+    b = np.ones(shards.size)
+    ctx.set_level_histograms(False)
+    try:
+        ctx.integrate_mixed_async(a, b, shards, N, 1e-9, first_slot=0, integrand=1)
+        got = [ctx.fetch(i) for i in range(shards.size)]
+    finally:
+        ctx.set_level_histograms(True)
+    want = {}
+    for s in range(N):
+        o = oracle.integrate_shard(s, N, G=ctx.num_workers // (96 * N), S=2, integrand=1, a=1e-4, b=1.0, eps=1e-9)
+        want[s] = (o.tasks, o.leaves)
+    for i, s in enumerate(shards):
+        assert (got[i].tasks, got[i].accepted) == want[int(s)], (i, int(s))
+    assert sum(want[s][0] for s in range(N)) == g["tasks"]
+
+
+def test_rccl_group_single_process(ctx, trees):
+    """aq_integrate_group over an in-library RCCL communicator (one GPU here: a group of one runs the
+    same grouped all-reduce / all-gather the 8-GPU node runs)."""
+    from ppls_amd import Group
+    with Group([ctx]) as grp:
+        assert grp.size == 1
+        for name in ["cosh4_eps1e-10", "sin_recip_eps1e-9", "gauss_eps1e-13"]:
+            g = trees[name]
+            r = grp.integrate(_problem(g))
+            assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"]), name
+            assert r.tasks_per_level == g["tasks_per_level"]
+            assert r.tasks_per_gpu == [g["tasks"]]
+            assert sum(r.tasks_per_cu.values()) == g["tasks"]
+            assert _area_ok(r.area, g["area_quad"])
+
+
+def test_rccl_group_join(ctx, trees):
+    """The one-process-per-GPU form (aq_group_unique_id + aq_group_join), as an MPI rank would use it."""
+    from ppls_amd import Group, Problem
+    uid = Group.unique_id()
+    with Group.join(ctx, 1, 0, uid) as grp:
+        r = grp.integrate(Problem(eps=1e-10, n_gpus=1))
+    g = trees["cosh4_eps1e-10"]
+    assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"])

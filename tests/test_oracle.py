@@ -134,3 +134,40 @@ def test_oracle_deep_eps(oracle):
     # verbatim replay of the reference's task arithmetic (it reproduced every MPI total)
     r = oracle.integrate(eps=1e-14)
     assert (r.tasks, r.leaves) == (30870291, 15435146)
+
+
+def test_plugin_fixture_pinned_by_reference(trees, plugin_bits):
+    """The AQ_F_USER plug-in's fixtures: the reference binary built with `#define F(arg)
+    exp(-(arg)*(arg))` printed the same task totals and Area= as the oracle's restatement."""
+    from oracle import pyoracle as O
+    for name in ["gauss_eps1e-10", "gauss_eps1e-13"]:
+        g = trees[name]
+        r = O.integrate(O.USER, g["a"], g["b"], g["eps"])
+        assert (r.tasks, r.leaves, r.levels) == (g["tasks"], g["leaves"], g["levels"])
+        assert g["reference"]["tasks_total"] == r.tasks == g["reference_p2"]["tasks_total"]
+        assert g["reference"]["area_printed"] == "%f" % r.area
+        assert g["reference_p2"]["area_printed"] == "%f" % r.area_lifo   # P=2: deterministic LIFO order
+    x = plugin_bits["x"].view(np.float64)
+    assert (O.F(x, O.USER).view(np.uint64) == plugin_bits["F"]).all()
+    assert (O.F(x, O.USER, O.HOST_LIBM).view(np.uint64) == plugin_bits["F"]).all()
+
+
+def test_exp_restatement_every_path_vs_host_libm():
+    """glibc exp restated for every path the plug-in surface exposes: tiny arguments, the main
+    range, |x| >= 512 with k > 0 and k < 0 (subnormal results), |x| >= 1024."""
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(17)
+    x = np.concatenate([rng.uniform(-745.2, -700, 100000), rng.uniform(-1100, -500, 50000),
+                        rng.uniform(-30, 30, 100000), rng.uniform(-1e-15, 1e-15, 5000), rng.uniform(500, 709.7, 50000),
+                        [0.0, -0.0, -708.39, -745.13, -745.14, -1024.0, -1e300, 2.0 ** -55, 5e-324, 709.78, 1e300]])
+    assert (O.exp(x).view(np.uint64) == O.exp(x, O.HOST_LIBM).view(np.uint64)).all()
+
+
+def test_deep_fixture_pinned_by_reference(deep_golden):
+    """eps=1e-14 (31 M tasks): the oracle reproduces the reference binary's task total (deep.json)."""
+    from oracle import pyoracle as O
+    g = deep_golden["cosh4_eps1e-14"]
+    r = O.integrate(eps=g["eps"], maxlev=128)
+    assert r.tasks == g["tasks"] == g["reference"]["tasks_total"]
+    assert (r.leaves, r.levels) == (g["leaves"], g["levels"])
+    assert abs(float(g["reference"]["area_printed"]) - r.area) <= 5e-7 + 1e-12 * r.area
