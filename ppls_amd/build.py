@@ -40,6 +40,17 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def build_variant(name, defines, verbose=False):
+    """An A/B variant of the library with extra -D flags: _build/libaquad_<name>.so (tools/ab.sh)."""
+    os.makedirs(OUT, exist_ok=True)
+    out = os.path.join(OUT, f"libaquad_{name}.so")
+    cmd = [HIPCC] + HIP_FLAGS + [f'-DAQ_USER_F_HEADER="{USER_F}"'] + list(defines) + ["-o", out] + SOURCES + LIBS
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return out
+
+
 def build(force=False, verbose=False):
     os.makedirs(OUT, exist_ok=True)
     tab = os.path.join(CSRC, "aq_exp_table.h")
@@ -61,5 +72,9 @@ def build(force=False, verbose=False):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
-    print("built", LIB)
+    if "--variant" in sys.argv:   # python ppls_amd/build.py --variant NAME [-DX=1 ...]
+        i = sys.argv.index("--variant")
+        print("built", build_variant(sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")]))
+    else:
+        build(force="--force" in sys.argv, verbose=True)
+        print("built", LIB)

@@ -151,6 +151,17 @@ __device__ __forceinline__ void masked_add(double& acc, double v, unsigned long 
         : "scc");
 }
 
+// m = max(m, v) on the lanes of `mask` only (one exec-masked v_max_u32).
+__device__ __forceinline__ void masked_max(unsigned& m, unsigned v, unsigned long long mask) {
+    unsigned long long saved;
+    asm("s_and_saveexec_b64 %1, %3\n\t"
+        "v_max_u32 %0, %0, %2\n\t"
+        "s_mov_b64 exec, %1"
+        : "+v"(m), "=&s"(saved)
+        : "v"(v), "s"(mask)
+        : "scc");
+}
+
 __device__ __forceinline__ void wave_sum_dd(double& hi, double& lo) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

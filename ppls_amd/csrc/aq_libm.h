@@ -13,6 +13,9 @@
 // The 2 KiB exp table lives in LDS (one ds_read_b128 per lookup); kernels stage it at entry
 // with aq_stage_exp_table().
 #pragma once
+#ifndef AQ_T2
+#define AQ_T2 0   // measured r02: 30.33 -> 30.49 ms per 8192-integral launch (longer dependency chain): off
+#endif
 #ifndef AQ_PIN_CONSTS
 #define AQ_PIN_CONSTS 1
 #endif
@@ -227,7 +230,7 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
 // FMA). A persistent kernel pins them in VGPRs once (pinned_exp_consts); the default instance lets
 // the compiler choose.
 struct ExpConsts {
-    double shift = kShift, c4 = kC4, c2 = kC2;
+    double shift = kShift + (AQ_T2 ? 128.0 : 0.0), c4 = kC4, c2 = kC2;   // (AQ_T2: see cosh_main_k)
     double inv = kInvLn2N, hi = kNegLn2hiN, lo = kNegLn2loN, c5 = kC5, c3 = kC3;
 };
 __device__ __forceinline__ ExpConsts pinned_exp_consts() {
@@ -246,6 +249,15 @@ __device__ __forceinline__ bool cosh_main_range(double x) {
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
     return ix >= 0x3fd62e43u && ix < 0x40360000u;
 }
+//
+// AQ_T2 (off by default, measured 0.5 % slower): the chains carry t2 = 2 * exp(|x|) instead of t. Rounding commutes with the exact
+// factor 2 in this range, so t2 = RN(2 scale * tmp + 2 scale) = 2 t, and
+//   RN(0.5 / t) = y3, the third Newton iterate of 1 / t2 from rcp(t2) (the compiler's quotient
+//   correction r = fma(-t, q, 0.5), fma(r, y, q) with q = 0.5 y is that step scaled by 2), and
+//   cosh = RN(0.5 t + RN(0.5 / t)) = fma(t2, 0.25, y3),
+// one multiply (q = 0.5 y) fewer per evaluation, bit for bit the same value. The doubled scale costs
+// nothing: with Shift + 128 in place of Shift, ki grows by 128 (index ki & 127 unchanged; the
+// subtraction kd - Shift unchanged) and (ki << 13) adds exactly 2^20 to the scale's high word.
 template <int K, bool CHECK = true>
 __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab,
                                             const ExpConsts& kk) {
@@ -282,6 +294,20 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
         t[k] = __fma_rn(scale, tmp[k], scale);
     }
     double y[K], q[K];
+#if AQ_T2
+    // t[k] holds 2 exp(|x|) here (kk.shift is Shift + 128, see above)
+#pragma unroll
+    for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) y[k] = __fma_rn(y[k], __fma_rn(-t[k], y[k], 1.0), y[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) c[k] = __fma_rn(t[k], 0.25, y[k]);   // 0.5*t + RN(0.5/t)
+    (void)q;
+    return out;
+#endif
 #pragma unroll
     for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
 #pragma unroll
@@ -308,11 +334,11 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 // A lane whose K points all lie in one interval [lo, hi] may pass range_hint = cosh_main_span(lo,
 // hi) (one test for the K points); -1 tests every point.
 __device__ __forceinline__ bool cosh_main_span(double lo, double hi) {
-    // lo >= 0 and both ends in the main range: every point between has a hi word between theirs
-    // (the word is monotonic for x >= 0), so glibc takes the exp path for all of them. Negative lo
-    // fails the unsigned test and goes to the per-point path.
-    constexpr uint32_t c0 = 0x3fd62e43u, span = 0x40360000u - 0x3fd62e43u;
-    return (hi_word(lo) - c0 < span) && (hi_word(hi) - c0 < span);
+    // lo >= 0.5*ln2 and hi < 22: every point between has a high word between theirs (the word is
+    // monotonic for x >= 0), so glibc takes the exp path for all of them. As SIGNED words a negative
+    // lo (sign bit set) is below 0x3fd62e43 and fails; then hi needs no lower test (hi >= lo). Two
+    // compares, no subtracts.
+    return ((int)hi_word(lo) >= 0x3fd62e43) && ((int)hi_word(hi) < 0x40360000);
 }
 template <int FID, int K>
 __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab,

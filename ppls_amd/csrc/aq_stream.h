@@ -259,6 +259,7 @@ struct Acc {
     double hi, lo;                  // double-double area (aq_device.h two_sum)
     unsigned tasks, leaves, maxd;   // per lane (seeding, mixed rounds)
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
+    unsigned maxdt;                 // per lane: largest pair word (depth | integral << 8) a round popped
 };
 
 // Flush a wave's accumulators for integral `tag` and reset them: the wave's double-double area (hi
@@ -274,7 +275,11 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     // the wave accumulates doubled areas for the built-in integrands (exact halving, aq_device.h)
     double hi = area_scale<FID>() * a.hi, lo = area_scale<FID>() * a.lo;
     wave_sum_dd(hi, lo);
-    const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul, m = wave_max_u(a.maxd);
+    // levels: the seeds' per-lane depth + 1, and the deepest popped pair (its depth byte + 1; one
+    // integral per ring, so the max over pair words is the max depth of that integral)
+    const unsigned mdt = wave_max_u(a.maxdt);
+    const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul,
+                   m = max(wave_max_u(a.maxd), mdt ? (mdt & 255u) + 1u : 0u);
     if (lane == 0 && t) {
         atomicAdd(&S.tasks, (unsigned long long)t);
         if constexpr (PCU) {
@@ -295,6 +300,7 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     a.hi = a.lo = 0.0;
     a.tasks = a.leaves = a.maxd = 0;
     a.ut = a.ul = 0;
+    a.maxdt = 0;
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
@@ -325,6 +331,17 @@ __device__ __forceinline__ void push_pair(double* s_pr, unsigned* s_dt, unsigned
     s_pr[2 * LREC + j] = fa; s_pr[3 * LREC + j] = fm; s_pr[4 * LREC + j] = fb;
 #endif
     s_dt[j] = dt;
+}
+
+// Raw LDS addressing for the round's pops and pushes. The five f64 fields of a slot sit LREC * 8 =
+// 26 KiB apart, so fm / fb lie beyond the 16-bit DS offset of the slot's base; through one opaque
+// second base (hi = base + 3 * 26 KiB) they become one ds_read2st64 / ds_write2st64 pair with
+// offsets 0 / 52, instead of two adds and two single accesses.
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ lds_f64* lds_at(unsigned byte_addr) { return (lds_f64*)(size_t)byte_addr; }
+__device__ __forceinline__ unsigned opaque(unsigned v) {
+    asm("" : "+v"(v));
+    return v;
 }
 
 // Ring slot of monotonic ring index i.
@@ -366,6 +383,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const unsigned bid = __builtin_amdgcn_readfirstlane(blockIdx.x);
     Ctl* __restrict__ qctl = P.ctls + P.first_slot;
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
+    const unsigned pr_base = (unsigned)(uintptr_t)s_pr;   // LDS byte offset of the pair block (low word of its flat address)
     const unsigned long long t_entry = rtc();
     stage_exp_table(tab, P.gtab);
     if (tid == 0) {
@@ -410,7 +428,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
     }
 
-    Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u};
+    Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u, 0u};
     // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
     for (unsigned i = lane; i < (unsigned)WCAP; i += 64) {
         const unsigned j = base + i;
@@ -980,80 +998,119 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }
         }
 
-        // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
-        //      tasks of a pair are evaluated together (two interleaved cosh chains)
-        unsigned long long c0 = 0, c1 = 0;
-        if constexpr (DIAG) c0 = clk();
-        const unsigned n = min(size, 64u);
-        const unsigned b0 = top - n;
-        const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
-        const bool act = lane < n;
-        // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
-        const unsigned j0 = base + ring_wrap(b0s + lane);
-        const double pa = s_a[j0], pb = s_b[j0], pfa = s_fa[j0], pfm = s_fm[j0], pfb = s_fb[j0];
-        const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
-        const unsigned dt = s_dt[j0];
-        const unsigned d = dt & 255u;
-        const int rtag = (int)(dt >> 8);
-        const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
-        Step2 st[2];
-        // both midpoints lie in [pa, pb]: one range test for the pair
-        task_step_k<FID, 2>(tl, tr, tfl, tfr, eps2, tab, st, kk, FID == F_COSH4 ? (int)cosh_main_span(pa, pb) : -1);
-        // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
-        // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
-        // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
-        const unsigned long long am = __ballot(act), dm = __ballot((int)d + 1 < max_depth);
-        const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
-        const unsigned long long okm = am & dm;
-        if (am & ~dm & (r0m | r1m)) err |= ERRB_DEPTH;
-        const bool ok = act && (int)d + 1 < max_depth;
-        const bool refine0 = ok && st[0].refine, refine1 = ok && st[1].refine;
-        const bool leaf0 = act && !st[0].refine, leaf1 = act && !st[1].refine;
-        // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
-        // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
-        // counts are wave-level, the area one masked add per accepted task.
-        const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
-        acc.ut += 2u * n;
-        acc.ul += (unsigned)__popcll(l0m) + (unsigned)__popcll(l1m);
-        acc.maxd = max(acc.maxd, act ? d + 1u : 0u);
-        // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-        masked_add(acc.hi, st[0].area2, l0m);   // doubled areas: halved at flush
-        masked_add(acc.hi, st[1].area2, l1m);
-        mixed |= (__ballot(rtag != tag) & am) != 0ull;     // the invariant, checked (error if broken)
-        if (HIST) {
-            if (act) {
-                atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
-                const unsigned nl = (leaf0 ? 1u : 0u) + (leaf1 ? 1u : 0u);
-                if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+        // ---- a burst of rounds: the hot loop. It runs while the ring neither empties nor nears
+        //      overflow, no cellar prefetch is in flight or due, and the next round is not a
+        //      give / poll check round: everything it touches besides the pairs is wave-uniform.
+        // the burst's state, re-asserted uniform (readfirstlane) once per burst: the outer loop's many
+        // paths leave the compiler unsure, and a "divergent" ring index turns every round's index
+        // arithmetic and the loop exit into VALU / exec-mask work
+        unsigned b_top = uni(top), b_size = uni(size), b_poll = uni(poll_ctr), b_ut = uni(acc.ut), b_ul = uni(acc.ul);
+        unsigned b_err = uni(err);
+        const unsigned b_bot = uni(bot), b_ctop = uni(ctop), b_pf = uni(pf_n);
+        bool b_mixed = uni(mixed);
+        for (;;) {
+            // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
+            //      tasks of a pair are evaluated together (two interleaved cosh chains)
+            unsigned long long c0 = 0, c1 = 0;
+            if constexpr (DIAG) c0 = clk();
+            const unsigned n = min(b_size, 64u);
+            const unsigned b0 = b_top - n;
+            const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
+            const bool act = lane < n;
+            // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
+            const unsigned j0 = base + ring_wrap(b0s + lane);
+            const unsigned a0 = pr_base + j0 * 8u;
+            const lds_f64* pl = lds_at(a0);
+            const lds_f64* ph = lds_at(opaque(a0 + 3u * LREC * 8u));
+            const double pa = pl[0], pb = pl[LREC], pfa = pl[2 * LREC], pfm = ph[0], pfb = ph[LREC];
+            const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
+            const unsigned dt = s_dt[j0];
+            const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
+            Step2 st[2];
+            // both midpoints lie in [pa, pb]: one range test for the pair
+            task_step_k<FID, 2>(tl, tr, tfl, tfr, eps2, tab, st, kk, FID == F_COSH4 ? (int)cosh_main_span(pa, pb) : -1);
+            // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
+            // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
+            // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
+            const unsigned long long am = __ballot(act), dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+            const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
+            const unsigned long long okm = am & dm;
+            if (am & ~dm & (r0m | r1m)) b_err |= ERRB_DEPTH;
+            // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
+            // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
+            // counts are wave-level, the area one masked add per accepted task.
+            const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
+            b_ut += 2u * n;
+            b_ul += (unsigned)__popcll(l0m) + (unsigned)__popcll(l1m);
+            masked_max(acc.maxdt, dt, am);
+            // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
+            masked_add(acc.hi, st[0].area2, l0m);   // doubled areas: halved at flush
+            masked_add(acc.hi, st[1].area2, l1m);
+            if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
+                                    // takes and seeds switch the tag); checked in diagnostic builds
+                const int rtag = (int)(dt >> 8);
+                b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
             }
-        }
-        if constexpr (DIAG) c1 = clk();
-        // each refining task pushes its children as one pair (:192-197)
-        const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-        const unsigned cnt0 = (unsigned)__popcll(mask0);
-        const unsigned cdt = dt + 1u;                       // depth + 1, same integral
-        if (refine0) {
-            const unsigned j = base + ring_wrap(b0s + mbcnt(mask0));
-            push_pair(s_pr, s_dt, j, pa, pm, pfa, st[0].fmid, pfm, cdt);
-        }
-        if (refine1) {
-            const unsigned j = base + ring_wrap(b0s + cnt0 + mbcnt(mask1));
-            push_pair(s_pr, s_dt, j, pm, pb, pfm, st[1].fmid, pfb, cdt);
-        }
-        top = b0 + cnt0 + (unsigned)__popcll(mask1);
-        if constexpr (DIAG) {
-            if (lane == 0) {
-                const unsigned long long c2 = clk();
-                atomicAdd(&s_dg[DG_ROUNDS], 1ull);
-                atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
-                atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
-                atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
-                atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)size);
-                atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
+            if (HIST) {
+                const unsigned d = dt & 255u;
+                if (__builtin_amdgcn_inverse_ballot_w64(am)) {
+                    atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                    const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
+                    if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+                }
             }
-            const unsigned nt = 2u * n;
-            if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
+            if constexpr (DIAG) c1 = clk();
+            // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
+            // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
+            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
+            const unsigned cnt0 = (unsigned)__popcll(mask0);
+            const unsigned cdt = dt + 1u;                       // depth + 1, same integral
+            if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
+                const unsigned j = base + ring_wrap(__builtin_amdgcn_mbcnt_hi((unsigned)(mask0 >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((unsigned)mask0, b0s)));
+                const unsigned aj = pr_base + j * 8u;
+                lds_f64* ql = lds_at(aj);
+                lds_f64* qh = lds_at(opaque(aj + 3u * LREC * 8u));
+                ql[0] = pa; ql[LREC] = pm; ql[2 * LREC] = pfa; qh[0] = st[0].fmid; qh[LREC] = pfm;
+                s_dt[j] = cdt;
+            }
+            if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
+                const unsigned j = base + ring_wrap(__builtin_amdgcn_mbcnt_hi((unsigned)(mask1 >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((unsigned)mask1, b0s + cnt0)));
+                const unsigned aj = pr_base + j * 8u;
+                lds_f64* ql = lds_at(aj);
+                lds_f64* qh = lds_at(opaque(aj + 3u * LREC * 8u));
+                ql[0] = pm; ql[LREC] = pb; ql[2 * LREC] = pfm; qh[0] = st[1].fmid; qh[LREC] = pfb;
+                s_dt[j] = cdt;
+            }
+            b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
+            if constexpr (DIAG) {
+                if (lane == 0) {
+                    const unsigned long long c2 = clk();
+                    atomicAdd(&s_dg[DG_ROUNDS], 1ull);
+                    atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
+                    atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
+                    atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
+                    atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
+                    atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
+                }
+                const unsigned nt = 2u * n;
+                if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
+            }
+            const unsigned sz = b_top - b_bot;
+            if (sz == 0u || sz > (unsigned)(WCAP - 64) || b_pf != 0u || (PREFETCH && b_ctop > 0u && sz <= (unsigned)PF_BELOW) ||
+                ((b_poll + 1u) % GIVE_ROUNDS) == 0u)
+                break;
+            ++b_poll;
+            b_size = sz;
+            __builtin_amdgcn_wave_barrier();
         }
+        top = b_top;
+        poll_ctr = b_poll;
+        acc.ut = b_ut;
+        acc.ul = b_ul;
+        err = b_err;
+        mixed = b_mixed;
         __builtin_amdgcn_wave_barrier();   // reconverge before the loop latch (keeps wave state uniform)
     }
 
