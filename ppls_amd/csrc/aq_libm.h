@@ -358,7 +358,11 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
                 if (!cosh_main_range(x[k])) c[k] = cosh_glibc(x[k], tab);
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) f[k] = c[k] * c[k] * c[k] * c[k];
+        for (int k = 0; k < K; ++k) f[k] = c[k] * c[k];           // ((c*c)*c)*c, stage by stage so
+#pragma unroll                                                        // the K chains interleave
+        for (int k = 0; k < K; ++k) f[k] = f[k] * c[k];
+#pragma unroll
+        for (int k = 0; k < K; ++k) f[k] = f[k] * c[k];
     } else if constexpr (FID == F_USER) {
 #pragma unroll
         for (int k = 0; k < K; ++k) f[k] = user::F(x[k], tab);

@@ -63,7 +63,7 @@ constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup dona
 #endif
 constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
 #ifndef AQ_GIVE_ROUNDS
-#define AQ_GIVE_ROUNDS 8    // with POLL_ROUNDS 64: 8 32.74, 16 32.63 ms, but 16 costs C3 eps=1e-3 6 % (19.5 -> 20.5 ms)
+#define AQ_GIVE_ROUNDS 32   // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
@@ -80,7 +80,13 @@ constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's 
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
-constexpr int PF_BELOW = WCAP - 128;   // below this ring size a wave prefetches 64 cellar pairs
+#ifndef AQ_PF_BELOW
+// r02 A/B (8192-integral launch, GIVE_ROUNDS 32): 112 28.39, 96 27.93, 80 27.57, 64 27.20, 48 28.18,
+// 32 30.25 ms, no prefetch 33.37 ms. The old 128 (= WCAP - 128) made a ring that had just spilled
+// its bottom 64 pairs (above 192) fetch the same 64 back a few rounds later: a ping-pong of one chunk.
+#define AQ_PF_BELOW (WCAP / 4)
+#endif
+constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetches 64 cellar pairs
 #ifndef AQ_PREFETCH
 #define AQ_PREFETCH 1
 #endif

@@ -14,7 +14,7 @@ for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
     per = collections.defaultdict(dict)
     names = {}
     for r in csv.DictReader(open(f)):
-        if "k_stream" not in r["Kernel_Name"] and "k_dfs" not in r["Kernel_Name"]:
+        if "k_stream" not in r["Kernel_Name"]:
             continue
         per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
         names[r["Dispatch_Id"]] = r["Kernel_Name"]
