@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1]): F(x)=cosh(x)^4 (aquadPartA.c:46) over [0,5] (:47-48) at
 EPSILON=1e-10 -- 1 464 273 tasks, 732 137 accepted subintervals per integral. One step = one batch
-of B (default 8192) such integrals through the hot path (persistent on-device farmer,
+of B (default 32768) such integrals through the hot path (persistent on-device farmer,
 ppls_amd/csrc/aq_stream.h). With N ranks (one process per GPU, torch.distributed backend "nccl" =
 RCCL) every integral is sharded: rank r evaluates shard r of N of each integral (the domain split
 into subranges per GPU; strong scaling, total work fixed), and a rank packs up to N batches into
@@ -103,7 +103,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8, help="timed batches")
     ap.add_argument("--warmup", type=int, default=2, help="untimed batches")
-    ap.add_argument("--batch", type=int, default=8192, help="integrals per step")
+    ap.add_argument("--batch", type=int, default=32768,
+                    help="integrals per step (one persistent launch per step on one GPU: ~0.5 ms of ramp-up and "
+                         "end-of-launch tail per launch, 2 %% of an 8192-integral launch, 0.5 %% of 32768)")
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true",

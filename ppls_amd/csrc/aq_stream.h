@@ -169,6 +169,8 @@ struct StreamParams {
     int shard, nshards;
     int D;                          // seed position depth
     int shares;                     // jobs per integral: job j = share j % shares of integral j / shares
+    int tail_from;                  // integrals from here on: tail_mult x shares each (nprob: none)
+    int tail_mult;
     unsigned epoch;                 // tags queue slots of this launch (ready[s] == epoch)
     unsigned qcap;                  // queue slots
     unsigned long long stall_ticks; // s_memrealtime ticks (100 MHz) a waiting leader tolerates WITHOUT
@@ -408,31 +410,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const double eps2 = doubled_areas<FID>() ? 2.0 * eps : eps;   // the rounds compare doubled areas (task_step_k)
     const int max_depth = P.max_depth;
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
-    unsigned shares = (unsigned)P.shares;
-    int D = P.D;
+    unsigned shares_main = (unsigned)P.shares;
+    int D_main = P.D;
     if (P.adaptive & 1) {
         const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
-            shares = h;
-            D = 63 - __builtin_clzll((unsigned long long)h * (unsigned long long)P.nshards) + S_W;
+            shares_main = h;
+            D_main = 63 - __builtin_clzll((unsigned long long)h * (unsigned long long)P.nshards) + S_W;
         }
     }
     const unsigned W = gridDim.x * (unsigned)NW;
     const unsigned w_all = bid * (unsigned)NW + wid;
-    const unsigned total_jobs = (unsigned)P.nprob * shares;
-    const unsigned V = shares * (unsigned)P.nshards;
-    const unsigned long long npos_total = 1ull << D;
-    const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per share (<= 8)
-    const unsigned nlev = (unsigned)D + 1u;                     // seeding evaluates depths 0..D
-    const unsigned nnodes = nlev * nb;
+    // the launch's last integrals (from tail_from on) are cut into tail_mult-times more, smaller
+    // shares: the jobs the waves draw last are short, so the waves run dry together instead of
+    // idling behind the longest last job (each integral keeps ONE partition: the counts are exact)
+    // (only where an integral is already several jobs: whole-integral jobs of tiny trees are short)
+    const unsigned tail_from = shares_main >= 8u ? (unsigned)P.tail_from : (unsigned)P.nprob;
+    const unsigned shares_tail = min(shares_main * (unsigned)P.tail_mult, W);
+    const int D_tail = 63 - __builtin_clzll((unsigned long long)shares_tail * (unsigned long long)P.nshards) + S_W;
+    const unsigned main_jobs = tail_from * shares_main;
+    const unsigned total_jobs = main_jobs + ((unsigned)P.nprob - tail_from) * shares_tail;
     const unsigned base = wid * WCAP;                            // this wave's ring
-    // seeding fast path (nnodes <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
-    unsigned long long colmask = 0;
-    if (nnodes <= 64) {
-        const unsigned kk = lane % nb;
-        for (unsigned d = 0; d < nlev; ++d)
-            if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
-    }
 
     Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u, 0u};
     // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
@@ -595,9 +593,26 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // ---- wave-local seeding of job `job` (see the file header)
                 unsigned long long cs = 0;
                 if constexpr (DIAG) cs = clk();
-                const int p = (int)(job / shares);
+                // the job's class: share `share` of integral p, cut into `shares` (its partition)
+                const bool in_tail = job >= main_jobs;
+                const unsigned shares = in_tail ? shares_tail : shares_main;
+                const int D = in_tail ? D_tail : D_main;
+                const unsigned jj = in_tail ? job - main_jobs : job;
+                const int p = (int)((in_tail ? tail_from : 0u) + jj / shares);
                 const unsigned shard_p = P.shard_of ? (unsigned)uni(P.shard_of[p]) : (unsigned)P.shard;
-                const unsigned vw = (job % shares) * (unsigned)P.nshards + shard_p;
+                const unsigned vw = (jj % shares) * (unsigned)P.nshards + shard_p;
+                const unsigned V = shares * (unsigned)P.nshards;
+                const unsigned long long npos_total = 1ull << D;
+                const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per share (<= 8)
+                const unsigned nlev = (unsigned)D + 1u;                     // seeding evaluates depths 0..D
+                const unsigned nnodes = nlev * nb;
+                // fast path (nnodes <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
+                unsigned long long colmask = 0;
+                if (nnodes <= 64) {
+                    const unsigned kk = lane % nb;
+                    for (unsigned d = 0; d < nlev; ++d)
+                        if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
+                }
                 if (p != tag) {
                     flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
                     tag = p;

@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     ctx = Context(0)
-    ctx.set_engine("stream")
     ctx.set_level_histograms(False)
     one = (np.zeros(1), np.full(1, 5.0))
     for _ in range(2):
