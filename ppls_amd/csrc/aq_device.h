@@ -192,6 +192,64 @@ __device__ __forceinline__ void wave_sum_dd(double& hi, double& lo) {
     }
 }
 
+// Full-wave reductions without LDS (every lane active): four DPP exchanges inside each row of 16
+// lanes (quad_perm xor 1, xor 2, half-row mirror, row mirror) leave every lane holding its row's
+// value, and the four rows combine through readlane. A __shfl_xor step is a ds_bpermute round trip
+// through LDS; a wave's exit flush made ~36 of them back to back (~2 us of a lone-integral launch).
+enum : int { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140 };
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = dpp_u<CTRL>((unsigned)b), hi = dpp_u<CTRL>((unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <typename Op>
+__device__ __forceinline__ unsigned wave_reduce_u(unsigned v, Op op) {
+    v = op(v, dpp_u<DPP_XOR1>(v));
+    v = op(v, dpp_u<DPP_XOR2>(v));
+    v = op(v, dpp_u<DPP_HALF_MIRROR>(v));
+    v = op(v, dpp_u<DPP_MIRROR>(v));
+    return op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+              op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ unsigned wave_add_full(unsigned v) {
+    return wave_reduce_u(v, [](unsigned x, unsigned y) { return x + y; });
+}
+__device__ __forceinline__ unsigned wave_max_full(unsigned v) {
+    return wave_reduce_u(v, [](unsigned x, unsigned y) { return x > y ? x : y; });
+}
+__device__ __forceinline__ unsigned wave_or_full(unsigned v) {
+    return wave_reduce_u(v, [](unsigned x, unsigned y) { return x | y; });
+}
+// double-double sum over the wave (every lane active); the result is wave-uniform
+__device__ __forceinline__ void wave_sum_dd_full(double& hi, double& lo) {
+    double h2 = dpp_d<DPP_XOR1>(hi), l2 = dpp_d<DPP_XOR1>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    h2 = dpp_d<DPP_XOR2>(hi); l2 = dpp_d<DPP_XOR2>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    h2 = dpp_d<DPP_HALF_MIRROR>(hi); l2 = dpp_d<DPP_HALF_MIRROR>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    h2 = dpp_d<DPP_MIRROR>(hi); l2 = dpp_d<DPP_MIRROR>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    double h0 = readlane_d(hi, 0), l0 = readlane_d(lo, 0), h1 = readlane_d(hi, 16), l1 = readlane_d(lo, 16);
+    double h3 = readlane_d(hi, 32), l3 = readlane_d(lo, 32);
+    const double h4 = readlane_d(hi, 48), l4 = readlane_d(lo, 48);
+    dd_add_dd(h0, l0, h1, l1);
+    dd_add_dd(h3, l3, h4, l4);
+    dd_add_dd(h0, l0, h3, l3);
+    hi = h0;
+    lo = l0;
+}
+
 // Wave-uniform values (readfirstlane). The persistent kernels' loops mix divergent regions with
 // wave-level state; LLVM's uniformity analysis loses track of that state across the joins and would
 // keep it in VGPRs, copied at every join. Re-asserting it once per iteration keeps it in SGPRs.

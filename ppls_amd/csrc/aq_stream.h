@@ -66,8 +66,26 @@ constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its vie
 #define AQ_GIVE_ROUNDS 32   // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
+// per-CU (lone-integral) launches: a wave's share of one integral lasts only a few to a few tens of
+// rounds, so it looks for idle siblings and starving workgroups far more often
+#ifndef AQ_KARG_PREFETCH
+#define AQ_KARG_PREFETCH 1
+#endif
+#ifndef AQ_GIVE_ROUNDS_PCU
+#define AQ_GIVE_ROUNDS_PCU 32
+#endif
+#ifndef AQ_POLL_ROUNDS_PCU
+#define AQ_POLL_ROUNDS_PCU 64
+#endif
+#ifndef AQ_GIVE_MIN_PCU
+#define AQ_GIVE_MIN_PCU 96
+#endif
+#ifndef AQ_LEAD_SLEEP
+#define AQ_LEAD_SLEEP 2     // s_sleep units (64 clocks) between a waiting leader's polls
+#endif
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
+constexpr unsigned SHARE_ROT = 1021;   // per-CU launches: share offset from one integral to the next
 constexpr int PCU_MAXK = 16;        // launches of fewer integrals keep per-workgroup (per-CU) counts
 constexpr int MAXK = 65536;         // max integrals per launch (tag: 24 bits of the pair's dt word)
 #ifndef AQ_GSPLIT_DEFAULT
@@ -92,13 +110,36 @@ constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetche
 #endif
 constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch (13 VGPRs)
 
-// Queue control block (HBM ticket queue), per-integral totals and histogram accumulators. One per
-// async slot; it must be all-zero when a launch starts -- the host zeroes slots lazily in batches.
-// q_tokens stores (tokens - G): the protocol's token count starts at G (every workgroup busy) and
-// the run is over when it reaches 0. jobs counts claimed jobs beyond the first W.
 struct alignas(128) Line {
     unsigned v;
     unsigned pad[31];
+};
+
+// One launch's HBM ticket queue and termination count (a line per word: pollers and atomics never
+// share a line). A context keeps two and its launches use them in turn; workgroup 0 of a launch
+// zeroes the one the next launch will use (a context's launches run in stream order), so every
+// launch starts from zeros without a reset of its own.
+//
+// Termination (token counting, two levels): the workgroups form NGROUP groups (workgroup b in group
+// b % NGROUP); idle[g] counts the idle workgroups of group g, and
+//   T = (groups with a busy workgroup) + sum over published, unconsumed chunks of (records + 1).
+// T starts at T0 = min(G, NGROUP) (tokens stores T - T0) and the run is over when T reaches 0. A
+// workgroup going idle adds 1 to its group's idle count; the one that makes the group all-idle takes
+// the group's token out of T. A workgroup taking a chunk (c records) subtracts 1 from its idle
+// count and adds (1 if the group was all-idle) - (c + 1) to T in one atomic. Every outstanding chunk
+// holds at least one token, so T stays positive while any chunk or busy workgroup exists: between a
+// group's 0 -> 1 busy transition and its T update, the taken chunk's own tokens are still counted.
+// The atomic that brings T to 0 is unique; its workgroup sets `done`, which the waiting leaders
+// poll. (One counter for all 256 workgroups made the final 256 idle transitions a ~3 us fan-in on
+// one line, then a poll of that same line by all of them.)
+constexpr int NGROUP = 8;
+struct QCtl {
+    Line tail;                 // chunk slots claimed by producers
+    Line head;                 // tickets taken by idle workgroups
+    Line tokens;               // T - T0
+    Line jobs;                 // job claims beyond the first W
+    Line done;                 // 1: T reached 0, every workgroup exits
+    Line idle[NGROUP];         // idle workgroups per group
 };
 // Per-integral totals: device-scope atomics at every flush (the farmer's `result += buff[0]`, :149,
 // and tasks_per_process, :162). The area is the exact fixed-point sum of the waves' double-double
@@ -106,22 +147,39 @@ struct alignas(128) Line {
 struct alignas(128) SlotSums {
     unsigned long long tasks, leaves, spilled;
     unsigned levels, error;
+    unsigned pcu;       // 1: a per-CU launch wrote this slot's counts as per-workgroup words (parts),
+                        // not into tasks / leaves / levels -- readers add them (slot_counts)
 };
+// Per-integral totals and histogram accumulators, one per async slot; all-zero when a launch starts
+// (the host zeroes used slots lazily, in batches).
 struct Ctl {
-    Line q_tail;               // chunk slots claimed by producers
-    Line q_head;               // tickets taken by idle workgroups
-    Line q_tokens;             // tokens - G
-    Line jobs;                 // job claims
     SlotSums sums;
     XSum area;                 // exact Σ of the accepted areas (larea + rarea, :199)
     unsigned long long hist[2 * AQ_MAX_LEVELS];   // [0,L): tasks per level, [L,2L): accepted per level
 };
 
-// Per-CU task counts of lone-integral (per-CU) launches: one word per (slot, workgroup), written once
-// by the workgroup's last wave: tasks << CU_BITS | hardware CU slot.
+// Counts of lone-integral (per-CU) launches: two words per (slot, workgroup), plain stores by the
+// workgroup's last wave -- [0] tasks << CU_BITS | hardware CU slot, [1] accepted << 8 | levels.
+// 256 workgroups adding three counters into one slot line at the same moment cost ~9 us of a 54 us
+// lone integral; readers sum the 256 words instead (slot_counts).
 constexpr int CU_BITS = 11;   // AQ_CU_SLOTS = 2048
 __host__ __device__ __forceinline__ unsigned long long pack_cu(unsigned long long tasks, unsigned cu) {
     return (tasks << CU_BITS) | (unsigned long long)(cu & ((1u << CU_BITS) - 1u));
+}
+struct Counts {
+    unsigned long long tasks, leaves;
+    unsigned levels;
+};
+__host__ __device__ __forceinline__ Counts slot_counts(const SlotSums& sm, const unsigned long long* wg_words, int grid) {
+    Counts c{sm.tasks, sm.leaves, sm.levels};
+    if (sm.pcu) {
+        for (int w = 0; w < grid; ++w) {
+            c.tasks += wg_words[2 * w] >> CU_BITS;
+            c.leaves += wg_words[2 * w + 1] >> 8;
+            c.levels = max(c.levels, (unsigned)(wg_words[2 * w + 1] & 255u));
+        }
+    }
+    return c;
 }
 
 // Exact accumulation into a slot's XSum (device atomics: any order, same bits).
@@ -175,8 +233,10 @@ struct StreamParams {
     unsigned qcap;                  // queue slots
     unsigned long long stall_ticks; // s_memrealtime ticks (100 MHz) a waiting leader tolerates WITHOUT
                                     // progress (queue head / tail / token count unchanged)
-    Ctl* ctls;                      // per-slot control blocks; the queue uses ctls[first_slot]
-    unsigned long long* parts;      // [slot * gridDim.x + wg]: pack_cu(tasks, cu), per-CU launches only
+    Ctl* ctls;                      // per-slot control blocks
+    QCtl* q;                        // this launch's queue and termination count (all-zero at launch)
+    QCtl* q_next;                   // the next launch's: workgroup 0 zeroes it
+    unsigned long long* parts;      // [2 * (slot * gridDim.x + wg) + 0/1]: per-CU launches' counts (slot_counts)
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
     Chunk* chunks;
     Cellar* cellar;                 // [gridDim.x * NW]
@@ -184,6 +244,8 @@ struct StreamParams {
     const ExpEntry* gtab;
     LaunchHint* hint;
     int per_cu;                     // also keep per-workgroup partials (per-CU task counts; lone integrals)
+    double2 kbounds[PCU_MAXK];      // per-CU launches: the bounds again, as kernel arguments (a scalar load
+                                    // with the launch's other arguments, not a cold HBM line at seeding)
     int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
 };
 
@@ -194,8 +256,9 @@ enum : int {
     DG_RECORDS_OUT, DG_T_WAIT, DG_LEADS, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
     DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
     DG_SEED_CALLS, DG_FLUSHES, DG_MIXED_ROUNDS, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_CELLAR_IN,
-    DG_CELLAR_OUT, DG_C_REFILL, DG_C_LOOP, DG_ACTIVE_TASKS, DG_PREFETCH, DG_PAD37, DG_PAD38, DG_PAD39,
-    DIAG_WORDS = 40
+    DG_CELLAR_OUT, DG_C_REFILL, DG_C_LOOP, DG_ACTIVE_TASKS, DG_PREFETCH, DG_T_INIT, DG_T_DONE, DG_T_FOLD,
+    DG_T_BROKE, DG_T_FLUSHED, DG_C_P1_CLASS, DG_C_P1_WALK, DG_C_P1_F, DG_T_SEED_IN, DG_T_CLASS, DG_PAD47,
+    DIAG_WORDS = 48
 };
 
 // Shared (LDS) state of one workgroup.
@@ -280,29 +343,32 @@ struct Acc {
 template <int FID, bool PCU>
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, WgState& S,
                                           unsigned long long* pc, XSum* px) {
-    // the wave accumulates doubled areas for the built-in integrands (exact halving, aq_device.h)
-    double hi = area_scale<FID>() * a.hi, lo = area_scale<FID>() * a.lo;
-    wave_sum_dd(hi, lo);
-    // levels: the seeds' per-lane depth + 1, and the deepest popped pair (its depth byte + 1; one
-    // integral per ring, so the max over pair words is the max depth of that integral)
-    const unsigned mdt = wave_max_u(a.maxdt);
-    const unsigned t = wave_sum_u(a.tasks) + a.ut, l = wave_sum_u(a.leaves) + a.ul,
-                   m = max(wave_max_u(a.maxd), mdt ? (mdt & 255u) + 1u : 0u);
-    if (lane == 0 && t) {
-        atomicAdd(&S.tasks, (unsigned long long)t);
-        if constexpr (PCU) {
-            atomicAdd(&pc[tag], (unsigned long long)t);
-            atomicAdd(&pc[PCU_MAXK + tag], (unsigned long long)l);
-            atomicMax(&pc[2 * PCU_MAXK + tag], (unsigned long long)m);
-            xs_atomic_add(px[tag].limb, hi);
-            xs_atomic_add(px[tag].limb, lo);
-        } else {
-            Ctl& c = P.ctls[P.first_slot + tag];
-            atomicAdd(&c.sums.tasks, (unsigned long long)t);
-            atomicAdd(&c.sums.leaves, (unsigned long long)l);
-            atomicMax(&c.sums.levels, m);
-            xs_atomic_add(c.area.limb, hi);
-            xs_atomic_add(c.area.limb, lo);
+    // a wave that ran no task of `tag` has nothing to add (idle waves at the exit of a lone launch)
+    if (uni(a.ut) != 0u || __ballot(a.tasks != 0u) != 0ull) {
+        // the wave accumulates doubled areas for the built-in integrands (exact halving, aq_device.h)
+        double hi = area_scale<FID>() * a.hi, lo = area_scale<FID>() * a.lo;
+        wave_sum_dd_full(hi, lo);
+        // levels: the seeds' per-lane depth + 1, and the deepest popped pair (its depth byte + 1; one
+        // integral per ring, so the max over pair words is the max depth of that integral)
+        const unsigned mdt = wave_max_full(a.maxdt);
+        const unsigned t = wave_add_full(a.tasks) + a.ut, l = wave_add_full(a.leaves) + a.ul,
+                       m = max(wave_max_full(a.maxd), mdt ? (mdt & 255u) + 1u : 0u);
+        if (lane == 0 && t) {
+            atomicAdd(&S.tasks, (unsigned long long)t);
+            if constexpr (PCU) {
+                atomicAdd(&pc[tag], (unsigned long long)t);
+                atomicAdd(&pc[PCU_MAXK + tag], (unsigned long long)l);
+                atomicMax(&pc[2 * PCU_MAXK + tag], (unsigned long long)m);
+                xs_atomic_add(px[tag].limb, hi);
+                xs_atomic_add(px[tag].limb, lo);
+            } else {
+                Ctl& c = P.ctls[P.first_slot + tag];
+                atomicAdd(&c.sums.tasks, (unsigned long long)t);
+                atomicAdd(&c.sums.leaves, (unsigned long long)l);
+                atomicMax(&c.sums.levels, m);
+                xs_atomic_add(c.area.limb, hi);
+                xs_atomic_add(c.area.limb, lo);
+            }
         }
     }
     a.hi = a.lo = 0.0;
@@ -389,11 +455,26 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // one read of the workgroup id: two reads merged after a divergent loop would be a "divergent"
     // phi, and through w_all / job every piece of wave state would follow it into VGPRs
     const unsigned bid = __builtin_amdgcn_readfirstlane(blockIdx.x);
-    Ctl* __restrict__ qctl = P.ctls + P.first_slot;
+    QCtl* __restrict__ qc = P.q;
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned pr_base = (unsigned)(uintptr_t)s_pr;   // LDS byte offset of the pair block (low word of its flat address)
-    const unsigned long long t_entry = rtc();
+    const unsigned long long t_entry = DIAG ? rtc() : 0ull;
+#if AQ_KARG_PREFETCH
+    // Bring every 64-B line of the kernel arguments into the scalar cache with ONE round trip: the
+    // compiler loads each field next to its first use, behind its own s_waitcnt, and every such
+    // first load missed to HBM (~900 cycles, 3072 waves on the same lines) -- five to eight of them
+    // in a row cost a lone launch ~3 us before its first seeding and ~2 us inside it.
+    {
+        const unsigned* kp = (const unsigned*)__builtin_amdgcn_kernarg_segment_ptr();
+        unsigned t = 0;
+#pragma unroll
+        for (unsigned o = 0; o < (unsigned)sizeof(StreamParams); o += 64) t += kp[o / 4];
+        asm volatile("" ::"s"(t));
+    }
+#endif
     stage_exp_table(tab, P.gtab);
+    if (bid == 0)
+        for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
     if (tid == 0) {
         S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1;
         S.exited = 0; S.tasks = 0;
@@ -405,6 +486,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
     __syncthreads();   // the only workgroup barrier before the exit
+    if constexpr (DIAG) { if (tid == 0) s_dg[DG_T_INIT] = rtc(); }
 
     const double eps = P.eps;
     const double eps2 = doubled_areas<FID>() ? 2.0 * eps : eps;   // the rounds compare doubled areas (task_step_k)
@@ -421,6 +503,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     }
     const unsigned W = gridDim.x * (unsigned)NW;
     const unsigned w_all = bid * (unsigned)NW + wid;
+    // termination group (QCtl): its workgroup count, and T0 = the number of groups
+    const unsigned grp = bid % (unsigned)NGROUP;
+    const unsigned grp_size = (gridDim.x - grp + (unsigned)NGROUP - 1u) / (unsigned)NGROUP;
+    const int t0 = (int)min(gridDim.x, (unsigned)NGROUP);
     // the launch's last integrals (from tail_from on) are cut into tail_mult-times more, smaller
     // shares: the jobs the waves draw last are short, so the waves run dry together instead of
     // idling behind the longest last job (each integral keeps ONE partition: the counts are exact)
@@ -441,14 +527,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
     Cellar* __restrict__ cel = P.cellar + w_all;
-    unsigned job = w_all;         // the job this wave seeds next (wave-uniform)
+    // the job this wave seeds next (wave-uniform). Per-CU launches number the waves transposed
+    // (wave wid of workgroup b seeds share wid * G + b): a workgroup's 12 shares then lie spread over
+    // the whole interval instead of side by side, so no workgroup holds only the costly end of it
+    unsigned job = PCU ? wid * gridDim.x + bid : w_all;
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
     unsigned claim = 0;           // lane 0: the prefetched claim
     unsigned err = 0;
     bool mixed = false;           // a round met pairs of another integral (never expected)
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
     bool counted_idle = false;
-    unsigned poll_ctr = wid * (POLL_ROUNDS / NW);
+    bool fresh = true;            // before this wave's first seeding
+    constexpr unsigned give_rounds = PCU ? AQ_GIVE_ROUNDS_PCU : GIVE_ROUNDS;
+    constexpr unsigned poll_rounds = PCU ? AQ_POLL_ROUNDS_PCU : POLL_ROUNDS;
+    constexpr unsigned give_min = PCU ? AQ_GIVE_MIN_PCU : GIVE_MIN;
+    unsigned poll_ctr = wid * (poll_rounds / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
     unsigned long long lock_spins = 0;
@@ -528,50 +621,57 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             unsigned k = 0;
             int ptag = 0;
             bool lead = false, seed = false;
-            int phase;
-            wave_lock(&S.lock, lane, lock_spins);
-            {
-                const unsigned avail = uni(S.ptop - S.pbot);
-                phase = uni(S.phase);
-                if (avail > 0) {
-                    k = min(avail, (unsigned)REFILL);
-                    const unsigned pb = S.pbot;
-                    // a ring holds pairs of ONE integral (the rounds count without per-lane tags):
-                    // take the leading run of pool pairs that share the first pair's integral
-                    ptag = (int)uni(s_dt[POOL0 + (pb & (PCAP - 1))] >> 8);
-                    for (unsigned q0 = 0; q0 < k; q0 += 64) {
-                        const unsigned q = q0 + lane;
-                        const unsigned long long bad =
-                            __ballot(q < k && (int)(s_dt[POOL0 + ((pb + q) & (PCAP - 1))] >> 8) != ptag);
-                        if (bad) {
-                            k = q0 + (unsigned)__builtin_ctzll(bad);
-                            break;
+            int phase = 0;
+            // a wave's first job needs no look at the pool (empty until some wave has run rounds):
+            // 12 waves would otherwise queue on the lock before their first F evaluation
+            if (fresh && job < total_jobs) {
+                seed = true;
+            } else {
+                wave_lock(&S.lock, lane, lock_spins);
+                {
+                    const unsigned avail = uni(S.ptop - S.pbot);
+                    phase = uni(S.phase);
+                    if (avail > 0) {
+                        k = min(avail, (unsigned)REFILL);
+                        const unsigned pb = S.pbot;
+                        // a ring holds pairs of ONE integral (the rounds count without per-lane tags):
+                        // take the leading run of pool pairs that share the first pair's integral
+                        ptag = (int)uni(s_dt[POOL0 + (pb & (PCAP - 1))] >> 8);
+                        for (unsigned q0 = 0; q0 < k; q0 += 64) {
+                            const unsigned q = q0 + lane;
+                            const unsigned long long bad =
+                                __ballot(q < k && (int)(s_dt[POOL0 + ((pb + q) & (PCAP - 1))] >> 8) != ptag);
+                            if (bad) {
+                                k = q0 + (unsigned)__builtin_ctzll(bad);
+                                break;
+                            }
+                        }
+                        for (unsigned i = lane; i < k; i += 64) copy_pair(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
+                        if (lane == 0) {
+                            S.pbot = pb + k;
+                            if (counted_idle) S.idle -= 1;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        counted_idle = false;
+                    } else if (job < total_jobs) {
+                        seed = true;
+                    } else {
+                        if (!counted_idle) {
+                            if (lane == 0) S.idle += 1;
+                            __builtin_amdgcn_wave_barrier();
+                            counted_idle = true;
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        if (phase == 0 && uni(S.idle) == NW) {   // every wave idle, pool empty, nothing to seed
+                            lead = true;
+                            if (lane == 0) S.phase = 1;
+                            __builtin_amdgcn_wave_barrier();
                         }
                     }
-                    for (unsigned i = lane; i < k; i += 64) copy_pair(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
-                    if (lane == 0) {
-                        S.pbot = pb + k;
-                        if (counted_idle) S.idle -= 1;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    counted_idle = false;
-                } else if (job < total_jobs) {
-                    seed = true;
-                } else {
-                    if (!counted_idle) {
-                        if (lane == 0) S.idle += 1;
-                        __builtin_amdgcn_wave_barrier();
-                        counted_idle = true;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (phase == 0 && uni(S.idle) == NW) {   // every wave idle, pool empty, nothing to seed
-                        lead = true;
-                        if (lane == 0) S.phase = 1;
-                        __builtin_amdgcn_wave_barrier();
-                    }
                 }
+                wave_unlock(&S.lock, lane);
             }
-            wave_unlock(&S.lock, lane);
+            fresh = false;
             if constexpr (DIAG) {
                 if (lane == 0) {
                     if (k) atomicAdd(&s_dg[DG_POOL_TAKE], (unsigned long long)k);
@@ -592,7 +692,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (seed) {
                 // ---- wave-local seeding of job `job` (see the file header)
                 unsigned long long cs = 0;
-                if constexpr (DIAG) cs = clk();
+                if constexpr (DIAG) {
+                    cs = clk();
+                    if (lane == 0) atomicMax(&s_dg[DG_T_SEED_IN], rtc());
+                }
                 // the job's class: share `share` of integral p, cut into `shares` (its partition)
                 const bool in_tail = job >= main_jobs;
                 const unsigned shares = in_tail ? shares_tail : shares_main;
@@ -600,7 +703,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned jj = in_tail ? job - main_jobs : job;
                 const int p = (int)((in_tail ? tail_from : 0u) + jj / shares);
                 const unsigned shard_p = P.shard_of ? (unsigned)uni(P.shard_of[p]) : (unsigned)P.shard;
-                const unsigned vw = (jj % shares) * (unsigned)P.nshards + shard_p;
+                unsigned sh = jj % shares;
+                // per-CU launches rotate the shares from one integral to the next: a wave whose share
+                // of one integral is costly gets another part of the next (static stride, no claims)
+                if (PCU) sh = (sh + (unsigned)p * SHARE_ROT) % shares;
+                const unsigned vw = sh * (unsigned)P.nshards + shard_p;
                 const unsigned V = shares * (unsigned)P.nshards;
                 const unsigned long long npos_total = 1ull << D;
                 const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per share (<= 8)
@@ -619,9 +726,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
                 // the bounds load goes out before the claim: waiting for it then leaves the claim (one
                 // contended atomic, not needed before the next job) in flight
-                const double2 ab = P.bounds[p];   // once per job (HBM / L2)
-                if (total_jobs > W) {
-                    if (lane == 0) claim = W + g_add(&qctl->jobs.v, 1u);   // next job: latency hides behind this one
+                const double2 ab = PCU ? P.kbounds[p] : P.bounds[p];   // once per job (HBM / L2)
+                if (PCU) {
+                    // per-CU launches cut every integral into one share per wave: wave w seeds share w of
+                    // each integral in turn (static stride, no claim). 3072 waves claiming through one
+                    // counter cost a 2-integral launch 87 us instead of ~25.
+                    job += W;
+                } else if (total_jobs > W) {
+                    if (lane == 0) claim = W + g_add(&qc->jobs.v, 1u);   // next job: latency hides behind this one
                     job_pending = true;
                 } else {
                     // every job was handed out at launch (job = w_all): no claim, so a lone integral's
@@ -644,6 +756,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (nnodes <= 64) {
                     // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
                     // decision; the first leaf depth of every position comes from ONE ballot
+                    unsigned long long ca = 0, cb = 0;
+                    if constexpr (DIAG) {
+                        ca = clk();
+                        if (lane == 0) atomicMax(&s_dg[DG_T_CLASS], rtc());
+                    }
                     const unsigned q = lane;
                     const bool isnode = q < nnodes;
                     const unsigned d = isnode ? q / nb : 0u, kk = isnode ? q - d * nb : 0u;
@@ -656,12 +773,20 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         if ((anc >> (d - 1 - i)) & 1ull) { l = mm; li = i * nb + kk; } else { r = mm; ri = i * nb + kk; }
                     }
                     mid = (l + r) / 2;                                        // :187
+                    if constexpr (DIAG) { asm volatile("" :: "v"(mid)); cb = clk(); }
                     const unsigned fq = nnodes + 2 <= 64 ? q : (q < nnodes ? q : 64u);
                     if (fq < nnodes + 2)
                         fmid = integrand<FID>(isnode ? mid : (q == nnodes ? A : B), tab);   // :188
                     if (fq < nnodes + 2) fm[q] = fmid;
                     if (nnodes + 2 > 64 && lane < 2) fm[nnodes + lane] = integrand<FID>(lane == 0 ? A : B, tab);
-                    if constexpr (DIAG) cp1 = clk();
+                    if constexpr (DIAG) {
+                        cp1 = clk();
+                        if (lane == 0) {
+                            atomicAdd(&s_dg[DG_C_P1_CLASS], ca - cs);
+                            atomicAdd(&s_dg[DG_C_P1_WALK], cb - ca);
+                            atomicAdd(&s_dg[DG_C_P1_F], cp1 - cb);
+                        }
+                    }
                     bool refine = false;
                     double leafarea = 0.0;
                     if (isnode) {
@@ -815,37 +940,44 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             int cmd = -1;   // >= 0 chunk slot, -1 exit, -2 error
             unsigned cnt = 0;
             if (lane == 0) {
+                bool last = false;   // this workgroup's idle transition ended the run
                 if (S.busy_token) {
-                    g_add((int*)&qctl->q_tokens.v, -1);
                     S.busy_token = 0;
+                    if (g_add(&qc->idle[grp].v, 1u) + 1u == grp_size)   // the group's last busy workgroup
+                        last = g_add((int*)&qc->tokens.v, -1) - 1 == -t0;
                 }
-                const unsigned h = g_add(&qctl->q_head.v, 1u);
-                // the wait is bounded by time WITHOUT PROGRESS, not since launch: while work exists,
-                // busy waves donate to waiting tickets within POLL_ROUNDS rounds, and every donation
-                // or idle / busy transition moves the token count or the queue tail
-                unsigned long long t_prog = rtc();
-                int seen_tk = 0;
-                unsigned seen_tl = ~0u;
-                for (unsigned spins = 0;; ++spins) {
-                    // both words are read every spin, issued together (one latency per spin)
-                    const unsigned rv = h < P.qcap ? ld_wt(&P.ready[(size_t)h * READY_STRIDE]) : 0u;
-                    const int tk = g_ld((int*)&qctl->q_tokens.v);
-                    if (rv == P.epoch) { cmd = (int)h; break; }
-                    if (tk == -(int)gridDim.x) { cmd = -1; break; }
-                    if ((spins & 63u) == 63u) {
-                        const unsigned tl = g_ld(&qctl->q_tail.v);
-                        const unsigned long long now = rtc();
-                        if (tk != seen_tk || tl != seen_tl) {
-                            seen_tk = tk;
-                            seen_tl = tl;
-                            t_prog = now;
-                        } else if (now - t_prog > P.stall_ticks) {
-                            err |= ERRB_TIMEOUT;
-                            cmd = -2;
-                            break;
+                if (last) {
+                    st_wt(&qc->done.v, 1u);
+                } else {
+                    const unsigned h = g_add(&qc->head.v, 1u);
+                    // the wait is bounded by time WITHOUT PROGRESS, not since launch: while work exists,
+                    // busy waves donate to waiting tickets within POLL_ROUNDS rounds, and every donation
+                    // or idle / busy transition moves the token count or the queue tail
+                    unsigned long long t_prog = rtc();
+                    int seen_tk = 0;
+                    unsigned seen_tl = ~0u;
+                    for (unsigned spins = 0;; ++spins) {
+                        // both words are read every spin, issued together (one latency per spin)
+                        const unsigned rv = h < P.qcap ? ld_wt(&P.ready[(size_t)h * READY_STRIDE]) : 0u;
+                        const unsigned dn = ld_wt(&qc->done.v);
+                        if (rv == P.epoch) { cmd = (int)h; break; }
+                        if (dn) { cmd = -1; break; }
+                        if ((spins & 63u) == 63u) {
+                            const int tk = g_ld((int*)&qc->tokens.v);
+                            const unsigned tl = g_ld(&qc->tail.v);
+                            const unsigned long long now = rtc();
+                            if (tk != seen_tk || tl != seen_tl) {
+                                seen_tk = tk;
+                                seen_tl = tl;
+                                t_prog = now;
+                            } else if (now - t_prog > P.stall_ticks) {
+                                err |= ERRB_TIMEOUT;
+                                cmd = -2;
+                                break;
+                            }
                         }
+                        __builtin_amdgcn_s_sleep(AQ_LEAD_SLEEP);
                     }
-                    __builtin_amdgcn_s_sleep(2);
                 }
                 if (cmd >= 0) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
@@ -854,6 +986,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             cmd = uni(__shfl(cmd, 0, 64));
             cnt = uni(__shfl(cnt, 0, 64));
+            if constexpr (DIAG) { if (lane == 0 && cmd < 0) atomicMax(&s_dg[DG_T_DONE], rtc()); }
             if (cmd < 0) {
                 wave_lock(&S.lock, lane, lock_spins);
                 if (lane == 0) S.phase = 2;
@@ -875,7 +1008,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 S.phase = 0;
                 S.busy_token = 1;
                 S.idle -= 1;   // the leader un-counts itself, so an empty chunk leads to a new leader
-                g_add((int*)&qctl->q_tokens.v, 1 - (int)cnt);
+                // busy again: the group's token comes back if the group was all-idle; the chunk's
+                // cnt + 1 tokens go (one atomic, so T never shows the chunk gone before the group back)
+                const bool was_all_idle = g_add(&qc->idle[grp].v, ~0u) == grp_size;
+                g_add((int*)&qc->tokens.v, (was_all_idle ? 1 : 0) - (int)(cnt + 1u));
             }
             counted_idle = false;
             wave_unlock(&S.lock, lane);
@@ -915,8 +1051,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // pool full: spill 64 pairs to an HBM chunk (tokens first, then publish)
                 unsigned slot = 0;
                 if (lane == 0) {
-                    slot = g_add(&qctl->q_tail.v, 1u);
-                    if (slot < P.qcap) g_add((int*)&qctl->q_tokens.v, 64);
+                    slot = g_add(&qc->tail.v, 1u);
+                    if (slot < P.qcap) g_add((int*)&qc->tokens.v, 64 + 1);   // records + 1 per chunk
                     spilled += 64;
                 }
                 slot = uni(__shfl(slot, 0, 64));
@@ -935,7 +1071,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
         ++poll_ctr;
         // ---- feed idle sibling waves
-        if ((poll_ctr % GIVE_ROUNDS) == 0 && size >= (unsigned)GIVE_MIN &&
+        if ((poll_ctr % give_rounds) == 0 && size >= give_min &&
             uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) > 0 &&
             uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
                 uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
@@ -957,17 +1093,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
         }
         // ---- donate to starving workgroups (another CU waits on the HBM queue)
-        if ((poll_ctr % POLL_ROUNDS) == 0) {
+        if ((poll_ctr % poll_rounds) == 0) {
             unsigned slot = 0xffffffffu;
             if (lane == 0) {
                 if ((int)(seen_head - seen_tail) > 0) {
                     unsigned expect = seen_tail;
-                    if (__hip_atomic_compare_exchange_strong(&qctl->q_tail.v, &expect, seen_tail + 1u, __ATOMIC_RELAXED,
+                    if (__hip_atomic_compare_exchange_strong(&qc->tail.v, &expect, seen_tail + 1u, __ATOMIC_RELAXED,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                         slot = seen_tail;
                 }
-                seen_head = g_ld(&qctl->q_head.v);
-                seen_tail = g_ld(&qctl->q_tail.v);
+                seen_head = g_ld(&qc->head.v);
+                seen_tail = g_ld(&qc->tail.v);
             }
             slot = uni(__shfl(slot, 0, 64));
             if (slot != 0xffffffffu) {
@@ -980,14 +1116,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if (pavail >= (unsigned)DONATE_MIN) {
                         k = min((unsigned)CH, pavail / 2u);
                         const unsigned pb = S.pbot;
-                        if (lane == 0) g_add((int*)&qctl->q_tokens.v, (int)k);
+                        if (lane == 0) g_add((int*)&qc->tokens.v, (int)k + 1);   // records + 1 per chunk
                         publish_chunk(P, R, slot, k, [&](unsigned i) { return POOL0 + ((pb + i) & (PCAP - 1)); }, lane);
                         if (lane == 0) S.pbot = pb + k;
                         wave_unlock(&S.lock, lane);
                     } else {
                         wave_unlock(&S.lock, lane);
                         k = size / 2u;   // may be 0: an empty chunk is harmless
-                        if (lane == 0) g_add((int*)&qctl->q_tokens.v, (int)k);
+                        if (lane == 0) g_add((int*)&qc->tokens.v, (int)k + 1);   // records + 1 per chunk
                         const unsigned b = bot;
                         publish_chunk(P, R, slot, k, [&](unsigned i) { return base + ring_slot(b + i); }, lane);
                         bot += k;
@@ -1120,7 +1256,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             const unsigned sz = b_top - b_bot;
             if (sz == 0u || sz > (unsigned)(WCAP - 64) || b_pf != 0u || (PREFETCH && b_ctop > 0u && sz <= (unsigned)PF_BELOW) ||
-                ((b_poll + 1u) % GIVE_ROUNDS) == 0u)
+                ((b_poll + 1u) % give_rounds) == 0u)
                 break;
             ++b_poll;
             b_size = sz;
@@ -1136,9 +1272,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     }
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
+    if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_BROKE], rtc()); }
     flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+    if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_FLUSHED], rtc()); }
     if (mixed) err |= ERRB_OVERFLOW;
-    const unsigned werr = wave_or_u(err);
+    const unsigned werr = wave_or_full(err);
     unsigned last_u = 0;
     if (lane == 0) {
         if (werr) {
@@ -1160,6 +1298,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         last_u = last ? 1u : 0u;
+        if constexpr (DIAG) { if (last) atomicMax(&s_dg[DG_T_FOLD], rtc()); }
         if (PCU && last) {
             // per-CU launch: this workgroup's counts per integral, once -- its per-CU word (a plain
             // store, one writer) and the slot sums (256 workgroups instead of every wave's flushes)
@@ -1168,13 +1307,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned long long t = __hip_atomic_load(&s_pc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned long long l = __hip_atomic_load(&s_pc[PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned m = (unsigned)__hip_atomic_load(&s_pc[2 * PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                P.parts[(size_t)(P.first_slot + p) * gridDim.x + bid] = pack_cu(t, cu);
-                Ctl& c = P.ctls[P.first_slot + p];
-                if (t) {
-                    atomicAdd(&c.sums.tasks, t);
-                    atomicAdd(&c.sums.leaves, l);
-                    atomicMax(&c.sums.levels, m);
-                }
+                unsigned long long* wp = P.parts + 2 * ((size_t)(P.first_slot + p) * gridDim.x + bid);
+                wp[0] = pack_cu(t, cu);
+                wp[1] = (l << 8) | (unsigned long long)(m & 255u);
+                if (bid == 0) P.ctls[P.first_slot + p].sums.pcu = 1u;
             }
         }
         if (last && (P.adaptive & 2)) {

@@ -284,37 +284,42 @@ __global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* o
 // Gather n slots' totals into a caller device buffer as f64 [area, tasks, accepted, error] rows,
 // ready for one collective (counts are exact in f64 below 2^53). One thread per slot: the area is
 // the correctly rounded value of the slot's exact accumulator.
-__global__ __launch_bounds__(64) void k_gather(const Ctl* __restrict__ ctls, int first, int n, int nslots,
-                                               double* __restrict__ out) {
+__global__ __launch_bounds__(64) void k_gather(const Ctl* __restrict__ ctls, const unsigned long long* __restrict__ parts,
+                                               int grid, int first, int n, int nslots, double* __restrict__ out) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i >= n) return;
-    const Ctl& c = ctls[(first + i) % nslots];
+    const int slot = (first + i) % nslots;
+    const Ctl& c = ctls[slot];
+    const Counts k = slot_counts(c.sums, parts + 2 * (size_t)slot * grid, grid);
     double* o = out + 4 * (size_t)i;
     o[0] = xs_round(c.area);
-    o[1] = (double)c.sums.tasks;
-    o[2] = (double)c.sums.leaves;
+    o[1] = (double)k.tasks;
+    o[2] = (double)k.leaves;
     o[3] = (double)c.sums.error;
 }
 
 // The same slots as exact int64 rows (AQ_EXACT_ROW each): limbs, tasks, accepted, spilled,
 // levels | error << 32. Sums of such rows (an int64 all-reduce) keep the area exact.
-__global__ __launch_bounds__(64) void k_gather_exact(const Ctl* __restrict__ ctls, int first, int n, int nslots,
-                                                     long long* __restrict__ out) {
+__global__ __launch_bounds__(64) void k_gather_exact(const Ctl* __restrict__ ctls,
+                                                     const unsigned long long* __restrict__ parts, int grid, int first,
+                                                     int n, int nslots, long long* __restrict__ out) {
     const int i = (int)blockIdx.x;
     if (i >= n) return;
-    const Ctl& c = ctls[(first + i) % nslots];
+    const int slot = (first + i) % nslots;
+    const Ctl& c = ctls[slot];
     long long* o = out + (size_t)AQ_EXACT_ROW * i;
     for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) o[k] = c.area.limb[k];
     if (threadIdx.x == 0) {
-        o[XS_LIMBS] = (long long)c.sums.tasks;
-        o[XS_LIMBS + 1] = (long long)c.sums.leaves;
+        const Counts k = slot_counts(c.sums, parts + 2 * (size_t)slot * grid, grid);
+        o[XS_LIMBS] = (long long)k.tasks;
+        o[XS_LIMBS + 1] = (long long)k.leaves;
         o[XS_LIMBS + 2] = (long long)c.sums.spilled;
-        o[XS_LIMBS + 3] = (long long)c.sums.levels | ((long long)c.sums.error << 32);
+        o[XS_LIMBS + 3] = (long long)k.levels | ((long long)c.sums.error << 32);
     }
 }
 
-// Return slots [first, first + n) to the all-zero state a launch needs: sums, the exact area
-// accumulator and the queue words; the histograms when they were written.
+// Return slots [first, first + n) to the all-zero state a launch needs: sums and the exact area
+// accumulator; the histograms when they were written.
 __global__ __launch_bounds__(128) void k_reset(Ctl* __restrict__ ctls, int first, int zero_hist) {
     Ctl& c = ctls[first + (int)blockIdx.x];
     for (int i = threadIdx.x; i < XS_LIMBS; i += blockDim.x) c.area.limb[i] = 0;
@@ -322,7 +327,6 @@ __global__ __launch_bounds__(128) void k_reset(Ctl* __restrict__ ctls, int first
         for (int i = threadIdx.x; i < 2 * AQ_MAX_LEVELS; i += blockDim.x) c.hist[i] = 0ull;
     if (threadIdx.x == 0) {
         c.sums = SlotSums{};
-        c.q_tail.v = 0u; c.q_head.v = 0u; c.q_tokens.v = 0u; c.jobs.v = 0u;
     }
 }
 
@@ -333,14 +337,16 @@ __global__ __launch_bounds__(256) void k_pack_group(const Ctl* __restrict__ ctls
                                                     int slot, int grid, int with_parts, long long* __restrict__ sum_row,
                                                     unsigned long long* __restrict__ info) {
     const Ctl& c = ctls[slot];
+    const unsigned long long* wp = parts + 2 * (size_t)slot * grid;
     for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) sum_row[k] = c.area.limb[k];
-    for (int k = threadIdx.x; k < grid; k += blockDim.x) info[3 + k] = with_parts ? parts[(size_t)slot * grid + k] : 0ull;
+    for (int k = threadIdx.x; k < grid; k += blockDim.x) info[3 + k] = with_parts ? wp[2 * k] : 0ull;
     if (threadIdx.x == 0) {
-        sum_row[XS_LIMBS] = (long long)c.sums.tasks;
-        sum_row[XS_LIMBS + 1] = (long long)c.sums.leaves;
+        const Counts k = slot_counts(c.sums, wp, grid);
+        sum_row[XS_LIMBS] = (long long)k.tasks;
+        sum_row[XS_LIMBS + 1] = (long long)k.leaves;
         sum_row[XS_LIMBS + 2] = (long long)c.sums.spilled;
-        info[0] = c.sums.tasks;
-        info[1] = c.sums.levels;
+        info[0] = k.tasks;
+        info[1] = k.levels;
         info[2] = c.sums.error;
     }
 }

@@ -23,10 +23,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--k", type=int, default=1, help="integrals per launch (k < 16: the per-CU instance)")
     args = ap.parse_args()
     ctx = Context(0)
     ctx.set_level_histograms(False)
-    one = (np.zeros(1), np.full(1, 5.0))
+    one = (np.zeros(args.k), np.full(args.k, 5.0))
     for _ in range(2):
         ctx.integrate_many_async(*one, args.eps)
     ctx.synchronize()
@@ -36,7 +37,7 @@ def main():
     ctx.synchronize()
     ms, n = ctx.kernel_time()
     ctx.kernel_timing(False)
-    out = {"eps": args.eps, "kernel_us_plain": ms * 1e3 / max(n, 1)}
+    out = {"eps": args.eps, "k": args.k, "kernel_us_plain": ms * 1e3 / max(n, 1)}
     ctx.set_diagnostics(True)
     ctx.kernel_timing(True)
     ctx.integrate_many_async(*one, args.eps)
@@ -48,14 +49,14 @@ def main():
     col = dict(zip(f, d.T.astype(np.float64)))
     t0 = col["t_start"].min()
     us = lambda k: (col[k] - t0) / 100.0   # s_memrealtime: 100 MHz
-    for k in ("t_start", "t_seeded", "t_last_round", "t_exit"):
+    for k in ("t_start", "t_init", "t_seed_in", "t_class", "t_seeded", "t_last_round", "t_done", "t_broke", "t_flushed", "t_fold", "t_exit"):
         out[k + "_us_q0_50_90_100"] = q(us(k))
     lead = col["t_first_lead"]
     ok = lead < 2 ** 63
     if ok.any():
         out["t_first_lead_us_q0_50_90_100"] = q((lead[ok] - t0) / 100.0)
     out["t_wait_us_per_wg_q"] = q(col["t_wait"] / 100.0)
-    for k in ("rounds", "seeds", "seed_calls", "active_lanes", "c_seed", "c_loop", "c_round", "leads"):
+    for k in ("rounds", "seeds", "seed_calls", "active_lanes", "c_seed", "c_seed_pass1", "c_seed_pass2", "c_seed_resolve", "c_p1_class", "c_p1_walk", "c_p1_f", "c_loop", "c_round", "leads"):
         if k in col:
             out[k + "_q0_50_90_100"] = q(col[k])
     out["tasks"] = float(col["tasks"].sum())
