@@ -88,12 +88,14 @@ def cpu_baseline(eps, target_s=12.0):
                                       f"{t_total:.1f} s"}
 
 
-def load_traffic():
-    """HBM bytes per launch of the persistent kernel from the committed PMC profile (or None)."""
+def load_traffic(tasks_per_launch):
+    """HBM bytes per launch of the persistent kernel: the committed PMC profile's bytes per task
+    (profiles/pmc_traffic.json, tools/profile_round.sh) times this launch's tasks (or None)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            per_task = json.load(f).get("hbm_bytes_per_task")
+        return per_task * tasks_per_launch if per_task else None
     except Exception:
         return None
 
@@ -272,7 +274,7 @@ def main():
             "single_integral_kernel_us": single_ms * 1e3 / single_n if single_n else None,
             "verified": ok,
             "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(),
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(tasks_per_launch),
                          "kernel": "aq::k_stream<0,false,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
                          "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": tasks_per_launch},
             "cpu_baseline": cpu,

@@ -184,6 +184,24 @@ __device__ __forceinline__ void masked_max(unsigned& m, unsigned v, unsigned lon
         : "scc");
 }
 
+// The round's three masked accumulations in one exec window: hi += a0 on the lanes of l0m, hi += a1
+// on l1m, m = max(m, v) on am -- exec saved once and restored once (5 SALU, not 6). Every mask is a
+// ballot taken under the current exec, so each is a subset of it.
+__device__ __forceinline__ void masked_acc3(double& hi, double a0, unsigned long long l0m, double a1,
+                                            unsigned long long l1m, unsigned& m, unsigned v, unsigned long long am) {
+    unsigned long long saved;
+    asm("s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, %5\n\t"
+        "v_add_f64 %0, %0, %3\n\t"
+        "s_mov_b64 exec, %6\n\t"
+        "v_add_f64 %0, %0, %4\n\t"
+        "s_mov_b64 exec, %7\n\t"
+        "v_max_u32 %2, %2, %8\n\t"
+        "s_mov_b64 exec, %1"
+        : "+v"(hi), "=&s"(saved), "+v"(m)
+        : "v"(a0), "v"(a1), "s"(l0m), "s"(l1m), "s"(am), "v"(v));
+}
+
 __device__ __forceinline__ void wave_sum_dd(double& hi, double& lo) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

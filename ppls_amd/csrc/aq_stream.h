@@ -45,10 +45,31 @@ namespace aq {
 constexpr int PT = AQ_PT;           // threads per workgroup
 constexpr int NW = PT / 64;         // waves (workers) per workgroup: 12, three per SIMD
 constexpr int WCAP = AQ_WCAP;       // per-wave LDS ring, pairs: a round pops <= 64, pushes <= 128
-constexpr int PCAP = 256;           // per-workgroup LDS pool ring, pairs (power of two)
-constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 3328 x 44 B = 143 KiB
+// LDS pair block, one field per array of LREC slots (SoA): a | b | fa | fm | fb, then the pair word
+// dt. AQ_LDS6: dt gets an 8-byte slot as a sixth field, so that with LREC = 50 x 64 every field of
+// a slot lies at 0 / 50 / 100 / 150 / 200 / 250 x 512 B from the slot's a -- inside the reach of
+// ds_read2st64 / ds_write2st64 offsets (8 bits of 512 B): a round's pop is three read2st64 and a
+// push three write2st64 from ONE address (no second base, no separate dt address). The pool shrinks
+// to 128 pairs to make room.
+#ifndef AQ_LDS6
+#define AQ_LDS6 1   // r02 A/B (8192 x eps=1e-10): 26.17 -> 25.85 ms per launch
+#endif
+#if AQ_LDS6
+constexpr int PCAP = 128;           // per-workgroup LDS pool ring, pairs (power of two)
+constexpr int DT_STRIDE = 2;        // dt words per slot (the low word of an 8-byte field)
+#else
+constexpr int PCAP = 256;
+constexpr int DT_STRIDE = 1;
+#endif
+constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots (3200 with AQ_LDS6: 150 KiB; else 3328 x 44 B = 143 KiB)
 constexpr int POOL0 = NW * WCAP;    // first pool slot
-constexpr int CH = 256;             // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
+constexpr int CH = PCAP;            // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
+// the pair words of the LDS block: slot j's word at p[DT_STRIDE * j]
+struct DtField {
+    unsigned* p;
+    __device__ __forceinline__ unsigned& operator[](unsigned j) const { return p[DT_STRIDE * j]; }
+    __device__ __forceinline__ DtField operator+(unsigned o) const { return DtField{p + DT_STRIDE * o}; }
+};
 #ifndef AQ_S_W
 #define AQ_S_W 2
 #endif
@@ -66,27 +87,19 @@ constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its vie
 #define AQ_GIVE_ROUNDS 32   // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
-// per-CU (lone-integral) launches: a wave's share of one integral lasts only a few to a few tens of
-// rounds, so it looks for idle siblings and starving workgroups far more often
-#ifndef AQ_KARG_PREFETCH
-#define AQ_KARG_PREFETCH 1
-#endif
-#ifndef AQ_GIVE_ROUNDS_PCU
-#define AQ_GIVE_ROUNDS_PCU 32
-#endif
-#ifndef AQ_POLL_ROUNDS_PCU
-#define AQ_POLL_ROUNDS_PCU 64
-#endif
-#ifndef AQ_GIVE_MIN_PCU
-#define AQ_GIVE_MIN_PCU 96
-#endif
+// (lone-integral launches, whose waves run only ~3-13 rounds of one share, measured with give /
+// poll intervals of 2-16 rounds and GIVE_MIN 32-64: all slower, 1e-10 up to 2x -- HBM donations
+// and bursts cut short cost more than the balance they buy; profiles/r02_ab)
 #ifndef AQ_LEAD_SLEEP
 #define AQ_LEAD_SLEEP 2     // s_sleep units (64 clocks) between a waiting leader's polls
 #endif
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
-constexpr unsigned SHARE_ROT = 1021;   // per-CU launches: share offset from one integral to the next
-constexpr int PCU_MAXK = 16;        // launches of fewer integrals keep per-workgroup (per-CU) counts
+constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from one integral to the next
+// launches of fewer integrals keep per-workgroup (per-CU) counts and LDS exact accumulators (AQ_LDS6
+// leaves LDS for 12 of them)
+constexpr int PCU_MAXK = AQ_LDS6 ? 12 : 16;
+constexpr int STATIC_MAXK = 16;     // launches of fewer integrals (unsharded): one share per wave, static stride
 constexpr int MAXK = 65536;         // max integrals per launch (tag: 24 bits of the pair's dt word)
 #ifndef AQ_GSPLIT_DEFAULT
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
@@ -244,6 +257,7 @@ struct StreamParams {
     const ExpEntry* gtab;
     LaunchHint* hint;
     int per_cu;                     // also keep per-workgroup partials (per-CU task counts; lone integrals)
+    int static_jobs;                // fewer than STATIC_MAXK integrals: static job stride (see k_stream)
     double2 kbounds[PCU_MAXK];      // per-CU launches: the bounds again, as kernel arguments (a scalar load
                                     // with the launch's other arguments, not a cold HBM line at seeding)
     int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
@@ -279,7 +293,7 @@ struct LdsPairs {
     double* fa;
     double* fm;
     double* fb;
-    unsigned* dt;
+    DtField dt;
 };
 
 __device__ __forceinline__ void wave_lock(int* lock, unsigned lane, unsigned long long& spins) {
@@ -378,35 +392,6 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
-// Write one pair into LDS slot j of the SoA block (a | b | fa | fm | fb, LREC doubles each). The
-// fields sit 52 x 512 B apart, so with AQ_ASM_PUSH all five go out from ONE address as
-// ds_write2st64 (a, b at 0/52), ds_write (fa at +53248) and ds_write2st64 (fm, fb at 156/208): the
-// compiler pairs only (a, b) and adds the fm / fb offsets (beyond the 16-bit DS offset) per push.
-// Writes only, so nothing waits on them here; LDS operations of one wave complete in order, so the
-// compiler's own later reads of the ring see them, and the "memory" clobber keeps its accesses on
-// their side of the asm.
-#ifndef AQ_ASM_PUSH
-#define AQ_ASM_PUSH 0
-#endif
-__device__ __forceinline__ void push_pair(double* s_pr, unsigned* s_dt, unsigned j, double a, double b, double fa,
-                                          double fm, double fb, unsigned dt) {
-#if AQ_ASM_PUSH
-    static_assert(LREC * 8 == 52 * 512, "push_pair's DS offsets assume 52 x 512 B per field");
-    const unsigned addr = (unsigned)(uintptr_t)(s_pr + j);   // low 32 bits of a flat LDS address = its offset
-    asm volatile(
-        "ds_write2st64_b64 %0, %1, %2 offset1:52\n\t"
-        "ds_write_b64 %0, %3 offset:53248\n\t"
-        "ds_write2st64_b64 %0, %4, %5 offset0:156 offset1:208"
-        :
-        : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb)
-        : "memory");
-#else
-    s_pr[j] = a; s_pr[LREC + j] = b;
-    s_pr[2 * LREC + j] = fa; s_pr[3 * LREC + j] = fm; s_pr[4 * LREC + j] = fb;
-#endif
-    s_dt[j] = dt;
-}
-
 // Raw LDS addressing for the round's pops and pushes. The five f64 fields of a slot sit LREC * 8 =
 // 26 KiB apart, so fm / fb lie beyond the 16-bit DS offset of the slot's base; through one opaque
 // second base (hi = base + 3 * 26 KiB) they become one ds_read2st64 / ds_write2st64 pair with
@@ -418,6 +403,40 @@ __device__ __forceinline__ unsigned opaque(unsigned v) {
     return v;
 }
 
+#if AQ_LDS6
+// One slot's six fields from / to ONE LDS address (the slot's a, in bytes): three ds_read2st64_b64
+// / ds_write2st64_b64 at 0 / 50 / 100 / 150 / 200 / 250 x 512 B (LREC = 3200 slots of 8 B per
+// field). The pop waits for its own reads (lgkmcnt(0)) inside the asm -- the compiler cannot count
+// LDS operations it does not see -- and the "memory" clobbers keep the compiler's own LDS accesses
+// on their side of both.
+static_assert(LREC * 8 == 50 * 512, "lds_pop6 / lds_push6 assume 50 x 512 B per field");
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void lds_pop6(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
+                                         unsigned& dt) {
+    f64x2 ab, ff, fd;
+    asm volatile(
+        "ds_read2st64_b64 %0, %3 offset1:50\n\t"
+        "ds_read2st64_b64 %1, %3 offset0:100 offset1:150\n\t"
+        "ds_read2st64_b64 %2, %3 offset0:200 offset1:250\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(ab), "=&v"(ff), "=&v"(fd)
+        : "v"(addr)
+        : "memory");
+    a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
+    dt = (unsigned)__double_as_longlong(fd.y);
+}
+__device__ __forceinline__ void lds_push6(unsigned addr, double a, double b, double fa, double fm, double fb,
+                                          unsigned dt) {
+    const double dw = __longlong_as_double((long long)dt);
+    asm volatile(
+        "ds_write2st64_b64 %0, %1, %2 offset1:50\n\t"
+        "ds_write2st64_b64 %0, %3, %4 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %0, %5, %6 offset0:200 offset1:250"
+        :
+        : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb), "v"(dw)
+        : "memory");
+}
+#endif
 // Ring slot of monotonic ring index i.
 __device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned)WCAP; }
 // Ring slot of b + k for a slot b < WCAP and k < WCAP: one mask (power-of-two ring) or one
@@ -436,8 +455,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
     // pair stores no midpoint: m = (a + b) / 2 is recomputed with the parent's own operands (:187),
     // bit-identical, so a pair is 44 B and a ring holds 256 pairs.
+#if AQ_LDS6
+    __shared__ double s_pr[6 * LREC];
+    const DtField s_dt{reinterpret_cast<unsigned*>(s_pr + 5 * LREC)};
+#else
     __shared__ double s_pr[5 * LREC];
-    __shared__ unsigned s_dt[LREC];
+    __shared__ unsigned s_dtw[LREC];
+    const DtField s_dt{s_dtw};
+#endif
     double* const s_a = s_pr;
     double* const s_b = s_pr + LREC;
     double* const s_fa = s_pr + 2 * LREC;
@@ -459,19 +484,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned pr_base = (unsigned)(uintptr_t)s_pr;   // LDS byte offset of the pair block (low word of its flat address)
     const unsigned long long t_entry = DIAG ? rtc() : 0ull;
-#if AQ_KARG_PREFETCH
-    // Bring every 64-B line of the kernel arguments into the scalar cache with ONE round trip: the
-    // compiler loads each field next to its first use, behind its own s_waitcnt, and every such
-    // first load missed to HBM (~900 cycles, 3072 waves on the same lines) -- five to eight of them
-    // in a row cost a lone launch ~3 us before its first seeding and ~2 us inside it.
-    {
-        const unsigned* kp = (const unsigned*)__builtin_amdgcn_kernarg_segment_ptr();
-        unsigned t = 0;
-#pragma unroll
-        for (unsigned o = 0; o < (unsigned)sizeof(StreamParams); o += 64) t += kp[o / 4];
-        asm volatile("" ::"s"(t));
-    }
-#endif
     stage_exp_table(tab, P.gtab);
     if (bid == 0)
         for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
@@ -527,10 +539,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
     Cellar* __restrict__ cel = P.cellar + w_all;
-    // the job this wave seeds next (wave-uniform). Per-CU launches number the waves transposed
-    // (wave wid of workgroup b seeds share wid * G + b): a workgroup's 12 shares then lie spread over
-    // the whole interval instead of side by side, so no workgroup holds only the costly end of it
-    unsigned job = PCU ? wid * gridDim.x + bid : w_all;
+    // the job this wave seeds next (wave-uniform). Launches of few integrals (static jobs) number the
+    // waves transposed (wave wid of workgroup b seeds share wid * G + b): a workgroup's 12 shares then
+    // lie spread over the whole interval instead of side by side, so no workgroup holds only the
+    // costly end of it
+    const bool static_jobs = PCU || P.static_jobs != 0;
+    unsigned job = static_jobs ? wid * gridDim.x + bid : w_all;
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
     unsigned claim = 0;           // lane 0: the prefetched claim
     unsigned err = 0;
@@ -538,9 +552,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
     bool counted_idle = false;
     bool fresh = true;            // before this wave's first seeding
-    constexpr unsigned give_rounds = PCU ? AQ_GIVE_ROUNDS_PCU : GIVE_ROUNDS;
-    constexpr unsigned poll_rounds = PCU ? AQ_POLL_ROUNDS_PCU : POLL_ROUNDS;
-    constexpr unsigned give_min = PCU ? AQ_GIVE_MIN_PCU : GIVE_MIN;
+    constexpr unsigned give_rounds = GIVE_ROUNDS, poll_rounds = POLL_ROUNDS, give_min = GIVE_MIN;
     unsigned poll_ctr = wid * (poll_rounds / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
@@ -704,9 +716,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const int p = (int)((in_tail ? tail_from : 0u) + jj / shares);
                 const unsigned shard_p = P.shard_of ? (unsigned)uni(P.shard_of[p]) : (unsigned)P.shard;
                 unsigned sh = jj % shares;
-                // per-CU launches rotate the shares from one integral to the next: a wave whose share
-                // of one integral is costly gets another part of the next (static stride, no claims)
-                if (PCU) sh = (sh + (unsigned)p * SHARE_ROT) % shares;
+                // static-job launches rotate the shares from one integral to the next: a wave whose
+                // share of one integral is costly gets another part of the next
+                if (static_jobs) sh = (sh + (unsigned)p * SHARE_ROT) % shares;
                 const unsigned vw = sh * (unsigned)P.nshards + shard_p;
                 const unsigned V = shares * (unsigned)P.nshards;
                 const unsigned long long npos_total = 1ull << D;
@@ -727,8 +739,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // the bounds load goes out before the claim: waiting for it then leaves the claim (one
                 // contended atomic, not needed before the next job) in flight
                 const double2 ab = PCU ? P.kbounds[p] : P.bounds[p];   // once per job (HBM / L2)
-                if (PCU) {
-                    // per-CU launches cut every integral into one share per wave: wave w seeds share w of
+                if (static_jobs) {
+                    // launches of few integrals cut every integral into one share per wave: wave w seeds share w of
                     // each integral in turn (static stride, no claim). 3072 waves claiming through one
                     // counter cost a 2-integral launch 87 us instead of ~25.
                     job += W;
@@ -743,7 +755,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const double A = ab.x, B = ab.y;
                 double* fm = s_a + base;          // [nnodes + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
                 double* leafa = s_b + base;       // [nnodes]: larea + rarea of node (d,k)
-                unsigned* flag = s_dt + base;     // [nnodes]: node (d,k) refines
+                const DtField flag = s_dt + base;  // [nnodes]: node (d,k) refines
                 auto position = [&](unsigned kk, bool& valid) -> unsigned long long {
                     const unsigned long long o = (kk & 1u) ? (unsigned long long)(V - 1 - vw) : (unsigned long long)vw;
                     const unsigned long long j = (unsigned long long)kk * V + o;
@@ -1161,11 +1173,22 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // the burst's state, re-asserted uniform (readfirstlane) once per burst: the outer loop's many
         // paths leave the compiler unsure, and a "divergent" ring index turns every round's index
         // arithmetic and the loop exit into VALU / exec-mask work
-        unsigned b_top = uni(top), b_size = uni(size), b_poll = uni(poll_ctr), b_ut = uni(acc.ut), b_ul = uni(acc.ul);
-        unsigned b_err = uni(err);
+        unsigned b_top = uni(top), b_size = uni(size), b_poll = uni(poll_ctr);
+        const unsigned b_top0 = b_top;
+        unsigned b_n = 0;                 // pairs popped in this burst (2 tasks each)
+        unsigned long long b_dv = 0;      // lanes that met the depth cap with a refining task
         const unsigned b_bot = uni(bot), b_ctop = uni(ctop), b_pf = uni(pf_n);
         bool b_mixed = uni(mixed);
-        for (;;) {
+        // the burst goes on while lo < size <= hi and the next round is no give / poll round:
+        // lo = PF_BELOW while the cellar holds pairs to prefetch (else 0: stop when empty), hi =
+        // WCAP - 64 (near overflow), or hi = lo while a prefetch is in flight (one round only).
+        // One subtract and one compare per round, and one compare for the round counter.
+        const unsigned b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
+        const unsigned b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
+        const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
+        unsigned b_r = 0;                                              // rounds run in this burst
+        bool b_go;
+        do {
             // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
             //      tasks of a pair are evaluated together (two interleaved cosh chains)
             unsigned long long c0 = 0, c1 = 0;
@@ -1177,11 +1200,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
             const unsigned j0 = base + ring_wrap(b0s + lane);
             const unsigned a0 = pr_base + j0 * 8u;
+#if AQ_LDS6
+            double pa, pb, pfa, pfm, pfb;
+            unsigned dt;
+            lds_pop6(a0, pa, pb, pfa, pfm, pfb, dt);
+#else
             const lds_f64* pl = lds_at(a0);
             const lds_f64* ph = lds_at(opaque(a0 + 3u * LREC * 8u));
             const double pa = pl[0], pb = pl[LREC], pfa = pl[2 * LREC], pfm = ph[0], pfb = ph[LREC];
-            const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
             const unsigned dt = s_dt[j0];
+#endif
+            const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
             const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
             Step2 st[2];
             // both midpoints lie in [pa, pb]: one range test for the pair
@@ -1189,20 +1218,22 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
             // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
             // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
+            // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
+            // measured 0.9 % slower)
             const unsigned long long am = __ballot(act), dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
             const unsigned long long okm = am & dm;
-            if (am & ~dm & (r0m | r1m)) b_err |= ERRB_DEPTH;
+            // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
+            const unsigned long long atcap = am & ~dm;
+            if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
             // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
             // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
             // counts are wave-level, the area one masked add per accepted task.
             const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
-            b_ut += 2u * n;
-            b_ul += (unsigned)__popcll(l0m) + (unsigned)__popcll(l1m);
-            masked_max(acc.maxdt, dt, am);
+            b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
             // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-            masked_add(acc.hi, st[0].area2, l0m);   // doubled areas: halved at flush
-            masked_add(acc.hi, st[1].area2, l1m);
+            // (doubled areas: halved at flush); the deepest pair popped, under the active mask
+            masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, dt, am);
             if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
                                     // takes and seeds switch the tag); checked in diagnostic builds
                 const int rtag = (int)(dt >> 8);
@@ -1226,19 +1257,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned j = base + ring_wrap(__builtin_amdgcn_mbcnt_hi((unsigned)(mask0 >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mask0, b0s)));
                 const unsigned aj = pr_base + j * 8u;
+#if AQ_LDS6
+                lds_push6(aj, pa, pm, pfa, st[0].fmid, pfm, cdt);
+#else
                 lds_f64* ql = lds_at(aj);
                 lds_f64* qh = lds_at(opaque(aj + 3u * LREC * 8u));
                 ql[0] = pa; ql[LREC] = pm; ql[2 * LREC] = pfa; qh[0] = st[0].fmid; qh[LREC] = pfm;
                 s_dt[j] = cdt;
+#endif
             }
             if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
                 const unsigned j = base + ring_wrap(__builtin_amdgcn_mbcnt_hi((unsigned)(mask1 >> 32),
                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mask1, b0s + cnt0)));
                 const unsigned aj = pr_base + j * 8u;
+#if AQ_LDS6
+                lds_push6(aj, pm, pb, pfm, st[1].fmid, pfb, cdt);
+#else
                 lds_f64* ql = lds_at(aj);
                 lds_f64* qh = lds_at(opaque(aj + 3u * LREC * 8u));
                 ql[0] = pm; ql[LREC] = pb; ql[2 * LREC] = pfm; qh[0] = st[1].fmid; qh[LREC] = pfb;
                 s_dt[j] = cdt;
+#endif
             }
             b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
             if constexpr (DIAG) {
@@ -1255,18 +1294,24 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
             }
             const unsigned sz = b_top - b_bot;
-            if (sz == 0u || sz > (unsigned)(WCAP - 64) || b_pf != 0u || (PREFETCH && b_ctop > 0u && sz <= (unsigned)PF_BELOW) ||
-                ((b_poll + 1u) % give_rounds) == 0u)
-                break;
-            ++b_poll;
             b_size = sz;
+            ++b_r;
+            // one compare: the give / poll round closes the size window (opaque, so the compiler does
+            // not split it back into two conditions joined by SALU selects)
+            unsigned span_r = b_r != b_max ? b_span : 0u;
+            asm("" : "+s"(span_r));
+            b_go = sz - b_lo1 < span_r;
             __builtin_amdgcn_wave_barrier();
-        }
+        } while (b_go);
+        b_poll += b_r - 1u;   // every round but the burst's last advances the give / poll counter
         top = b_top;
         poll_ctr = b_poll;
-        acc.ut = b_ut;
-        acc.ul = b_ul;
-        err = b_err;
+        // every refining task pushed one pair, so pushes = (b_top - b_top0) + b_n and the accepted
+        // tasks are 2 b_n - pushes = b_n - (b_top - b_top0) (a burst that met the depth cap dropped
+        // tasks as well: those count as accepted here, and the launch reports ERRB_DEPTH)
+        acc.ut += 2u * b_n;
+        acc.ul += b_n - (b_top - b_top0);
+        if (b_dv) err |= ERRB_DEPTH;
         mixed = b_mixed;
         __builtin_amdgcn_wave_barrier();   // reconverge before the loop latch (keeps wave state uniform)
     }

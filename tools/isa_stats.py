@@ -60,24 +60,53 @@ def main():
     i = s.index(a.kernel + ":")
     j = s.index(".Lfunc_end", i)
     body = s[i:j].split("\n")
-    # loops: a label line "...: ; ... Loop Header: Depth=k" and a backedge branch to it
-    labels = {}
-    for n, ln in enumerate(body):
-        m = re.match(r"^(\.LBB\d+_\d+):", ln)
+    # blocks: a label line ".LBBx_y:" with LLVM's loop comment ("Loop Header: Depth=k" or "in Loop:
+    # Header=BBx_z Depth=k"); the round's loop is the innermost loop whose blocks hold the v_rcp_f64 of
+    # the division, a v_mbcnt_lo and a ds_read2st64 -- counted over ALL its blocks (a rotated loop
+    # places some of them after its back-edge)
+    blocks = []   # (label, header_of_loop_or_None, depth, lines)
+    cur = None
+    for ln in body:
+        m = re.match(r"^(\.LBB(\d+_\d+)):(.*)$", ln)
         if m:
-            labels[m.group(1)] = n
+            hdr, depth = None, 0
+            mh = re.search(r"Loop Header: Depth=(\d+)", m.group(3))
+            mi = re.search(r"in Loop: Header=BB(\d+_\d+) Depth=(\d+)", m.group(3))
+            if mh:
+                hdr, depth = m.group(2), int(mh.group(1))
+            elif mi:
+                hdr, depth = mi.group(1), int(mi.group(2))
+            cur = [m.group(1), hdr, depth, []]
+            blocks.append(cur)
+        elif cur is not None:
+            mh = re.search(r"Loop Header: Depth=(\d+)", ln)
+            if mh and ln.strip().startswith(";") and not any(x.strip() and not x.strip().startswith(";") for x in cur[3]):
+                cur[1], cur[2] = cur[0][4:], int(mh.group(1))   # "; => This Inner Loop Header" under the label
+            cur[3].append(ln)
+    inloop = lambda b, key: b[1] == key[0] and b[2] >= key[1]
+    keys = {(b[1], b[2]) for b in blocks if b[1]}
     best = None
-    for n, ln in enumerate(body):
-        m = re.match(r"^\s+s_(?:cbranch_\w+|branch)\s+(\.LBB\d+_\d+)", ln)
-        if m and m.group(1) in labels and labels[m.group(1)] < n:
-            lo, hi = labels[m.group(1)], n
-            seg = body[lo:hi + 1]
-            if any("v_rcp_f64" in x for x in seg) and any("v_mbcnt_lo" in x for x in seg) and any("ds_read2st64" in x for x in seg):
-                if best is None or hi - lo < best[1] - best[0]:
-                    best = (lo, hi)
+    for key in keys:
+        lines = [x for b in blocks if inloop(b, key) for x in b[3]]
+        if any("v_rcp_f64" in x for x in lines) and any("v_mbcnt_lo" in x for x in lines) and any("ds_read2st64" in x for x in lines):
+            if best is None or key[1] > best[1]:
+                best = key
     if best is None:
         sys.exit("no loop with v_rcp_f64 found")
-    seg = [x for x in body[best[0]:best[1] + 1] if re.match(r"^\s+[a-z]", x) and not x.strip().startswith(";")]
+    # the hot path: the contiguous run of the loop's blocks around its header (a rotated loop's latch
+    # sits just before the header), up to the last back-edge; out-of-line blocks (the cosh_glibc
+    # fallback) lie beyond it
+    h = next(i for i, b in enumerate(blocks) if b[0][4:] == best[0])
+    lo = h
+    while lo > 0 and inloop(blocks[lo - 1], best):
+        lo -= 1
+    hi = h
+    while hi + 1 < len(blocks) and inloop(blocks[hi + 1], best):
+        hi += 1
+    heads = "|".join(re.escape(b[0]) for b in blocks[lo:h + 1])   # the latch run and the header
+    last = max(i for i in range(h, hi + 1) if any(re.search(r"s_(cbranch_\w+|branch)\s+(" + heads + r")\b", x) for x in blocks[i][3]))
+    seg = [x for b in blocks[lo:last + 1] for x in [b[0] + ":"] + b[3]]
+    seg = [x for x in seg if re.match(r"^\s+[a-z]", x) and not x.strip().startswith(";")]
     counts = {}
     for x in seg:
         c = classify(x.strip())
@@ -86,10 +115,10 @@ def main():
     for key in ("VGPRs", "TotalSGPRs", "ScratchSize", "Occupancy", "LDS Size"):
         m = re.search(re.escape(a.kernel) + r".*?" + re.escape(key) + r"[^:]*: (\d+)", remarks, re.S)
         res[key] = m.group(1) if m else "?"
-    print("kernel", a.kernel, "loop lines", best, "resources", res)
+    print("kernel", a.kernel, "loop header BB%s depth %d" % best, "resources", res)
     print("instructions:", len(seg), counts, "VALU total", counts.get("valu_f64", 0) + counts.get("valu_other", 0))
     if a.dump:
-        print("\n".join(body[best[0]:best[1] + 1]))
+        print("\n".join(seg))
 
 
 if __name__ == "__main__":
