@@ -95,7 +95,8 @@ __host__ __device__ constexpr double area_scale() { return doubled_areas<FID>() 
 template <int FID, int K>
 __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (&r)[K], const double (&fl)[K],
                                             const double (&fr)[K], double eps2, const ExpEntry* __restrict__ tab,
-                                            Step2 (&s)[K], const ExpConsts& kk = ExpConsts{}, int range_hint = -1) {
+                                            Step2 (&s)[K], const ExpConsts& kk = ExpConsts{}, int range_hint = -1,
+                                            unsigned long long out_mask = 0ull) {
     double mid[K], fmid[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) mid[k] = (l[k] + r[k]) / 2;   // :187
@@ -112,7 +113,7 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
         asm volatile("" : "+v"(lr2e[k]), "+v"(wl[k]), "+v"(wr[k]));
     }
 #endif
-    integrand_k<FID, K>(mid, fmid, tab, kk, range_hint);       // :188
+    integrand_k<FID, K>(mid, fmid, tab, kk, range_hint, out_mask);   // :188
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         if constexpr (doubled_areas<FID>()) {
@@ -185,8 +186,8 @@ __device__ __forceinline__ void masked_max(unsigned& m, unsigned v, unsigned lon
 }
 
 // The round's three masked accumulations in one exec window: hi += a0 on the lanes of l0m, hi += a1
-// on l1m, m = max(m, v) on am -- exec saved once and restored once (5 SALU, not 6). Every mask is a
-// ballot taken under the current exec, so each is a subset of it.
+// on l1m, m = max(m, low byte of v) on am -- exec saved once and restored once (5 SALU, not 6).
+// Every mask is a ballot taken under the current exec, so each is a subset of it.
 __device__ __forceinline__ void masked_acc3(double& hi, double a0, unsigned long long l0m, double a1,
                                             unsigned long long l1m, unsigned& m, unsigned v, unsigned long long am) {
     unsigned long long saved;
@@ -196,7 +197,7 @@ __device__ __forceinline__ void masked_acc3(double& hi, double a0, unsigned long
         "s_mov_b64 exec, %6\n\t"
         "v_add_f64 %0, %0, %4\n\t"
         "s_mov_b64 exec, %7\n\t"
-        "v_max_u32 %2, %2, %8\n\t"
+        "v_max_u32_sdwa %2, %2, %8 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
         "s_mov_b64 exec, %1"
         : "+v"(hi), "=&s"(saved), "+v"(m)
         : "v"(a0), "v"(a1), "s"(l0m), "s"(l1m), "s"(am), "v"(v));

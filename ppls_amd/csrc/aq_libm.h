@@ -332,7 +332,8 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 
 // F at K independent points (one round of K records per lane); every lane of the wave calls it.
 // A lane whose K points all lie in one interval [lo, hi] may pass range_hint = cosh_main_span(lo,
-// hi) (one test for the K points); -1 tests every point.
+// hi) (one test for the K points); -1 tests every point; 2: out_mask is the wave mask of the lanes
+// whose points may lie outside the exp path (the caller's one test per lane).
 __device__ __forceinline__ bool cosh_main_span(double lo, double hi) {
     // lo >= 0.5*ln2 and hi < 22: every point between has a high word between theirs (the word is
     // monotonic for x >= 0), so glibc takes the exp path for all of them. As SIGNED words a negative
@@ -342,11 +343,20 @@ __device__ __forceinline__ bool cosh_main_span(double lo, double hi) {
 }
 template <int FID, int K>
 __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab,
-                                            const ExpConsts& kk = ExpConsts{}, int range_hint = -1) {
+                                            const ExpConsts& kk = ExpConsts{}, int range_hint = -1,
+                                            unsigned long long out_mask = 0ull) {
     if constexpr (FID == F_COSH4) {
         double c[K];
         bool out;
-        if (range_hint >= 0) {
+        if (range_hint == 2) {
+            cosh_main_k<K, false>(x, c, tab, kk);
+            if (__builtin_expect(out_mask != 0ull, 0)) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (!cosh_main_range(x[k])) c[k] = cosh_glibc(x[k], tab);
+            }
+            out = false;
+        } else if (range_hint >= 0) {
             cosh_main_k<K, false>(x, c, tab, kk);
             out = range_hint == 0;
         } else {

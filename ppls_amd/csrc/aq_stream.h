@@ -45,23 +45,16 @@ namespace aq {
 constexpr int PT = AQ_PT;           // threads per workgroup
 constexpr int NW = PT / 64;         // waves (workers) per workgroup: 12, three per SIMD
 constexpr int WCAP = AQ_WCAP;       // per-wave LDS ring, pairs: a round pops <= 64, pushes <= 128
-// LDS pair block, one field per array of LREC slots (SoA): a | b | fa | fm | fb, then the pair word
-// dt. AQ_LDS6: dt gets an 8-byte slot as a sixth field, so that with LREC = 50 x 64 every field of
-// a slot lies at 0 / 50 / 100 / 150 / 200 / 250 x 512 B from the slot's a -- inside the reach of
-// ds_read2st64 / ds_write2st64 offsets (8 bits of 512 B): a round's pop is three read2st64 and a
-// push three write2st64 from ONE address (no second base, no separate dt address). The pool shrinks
-// to 128 pairs to make room.
-#ifndef AQ_LDS6
-#define AQ_LDS6 1   // r02 A/B (8192 x eps=1e-10): 26.17 -> 25.85 ms per launch
-#endif
-#if AQ_LDS6
+// LDS pair block, one field per array of LREC slots (SoA): a | b | fa | fm | fb | dt, the pair word
+// dt in the low half of an 8-byte field. With LREC = 50 x 64 every field of a slot lies at 0 / 50 /
+// 100 / 150 / 200 / 250 x 512 B from the slot's a -- inside the reach of ds_read2st64 /
+// ds_write2st64 offsets (8 bits of 512 B): a round's pop is three read2st64 and a push three
+// write2st64 from ONE address (r02 A/B, 8192 x eps=1e-10: 26.17 -> 25.85 ms per launch against
+// five fields + a 4-byte dt array, which needed a second base for fm / fb and a dt address per
+// access; the pool went from 256 to 128 pairs to make room).
 constexpr int PCAP = 128;           // per-workgroup LDS pool ring, pairs (power of two)
 constexpr int DT_STRIDE = 2;        // dt words per slot (the low word of an 8-byte field)
-#else
-constexpr int PCAP = 256;
-constexpr int DT_STRIDE = 1;
-#endif
-constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots (3200 with AQ_LDS6: 150 KiB; else 3328 x 44 B = 143 KiB)
+constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 3200 x 48 B = 150 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = PCAP;            // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
 // the pair words of the LDS block: slot j's word at p[DT_STRIDE * j]
@@ -96,11 +89,17 @@ constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle sibli
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from one integral to the next
-// launches of fewer integrals keep per-workgroup (per-CU) counts and LDS exact accumulators (AQ_LDS6
-// leaves LDS for 12 of them)
-constexpr int PCU_MAXK = AQ_LDS6 ? 12 : 16;
+// launches of fewer integrals keep per-workgroup (per-CU) counts and LDS exact accumulators (the LDS
+// left beside the pair block holds 12)
+constexpr int PCU_MAXK = 12;
 constexpr int STATIC_MAXK = 16;     // launches of fewer integrals (unsharded): one share per wave, static stride
-constexpr int MAXK = 65536;         // max integrals per launch (tag: 24 bits of the pair's dt word)
+constexpr int MAXK = 65536;         // max integrals per launch (tag: the pair word's high 16 bits)
+// The pair word dt: bits 0-7 the pair's depth (the depth of its two tasks), bit 8 SPAN_BIT, bits
+// 16-31 the integral (tag). SPAN_BIT (cosh4): the pair's interval lies where glibc's cosh takes its
+// exp path (cosh_main_span) -- set at seeding, inherited by the children (sub-intervals), so a
+// round tests one byte instead of two words.
+constexpr unsigned SPAN_BIT = 1u << 8;
+constexpr int TAG_SHIFT = 16;
 #ifndef AQ_GSPLIT_DEFAULT
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
@@ -344,7 +343,7 @@ struct Acc {
     double hi, lo;                  // double-double area (aq_device.h two_sum)
     unsigned tasks, leaves, maxd;   // per lane (seeding, mixed rounds)
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
-    unsigned maxdt;                 // per lane: largest pair word (depth | integral << 8) a round popped
+    unsigned maxdt;                 // per lane: the deepest pair depth (dt's low byte) a round popped
 };
 
 // Flush a wave's accumulators for integral `tag` and reset them: the wave's double-double area (hi
@@ -392,18 +391,6 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
-// Raw LDS addressing for the round's pops and pushes. The five f64 fields of a slot sit LREC * 8 =
-// 26 KiB apart, so fm / fb lie beyond the 16-bit DS offset of the slot's base; through one opaque
-// second base (hi = base + 3 * 26 KiB) they become one ds_read2st64 / ds_write2st64 pair with
-// offsets 0 / 52, instead of two adds and two single accesses.
-typedef __attribute__((address_space(3))) double lds_f64;
-__device__ __forceinline__ lds_f64* lds_at(unsigned byte_addr) { return (lds_f64*)(size_t)byte_addr; }
-__device__ __forceinline__ unsigned opaque(unsigned v) {
-    asm("" : "+v"(v));
-    return v;
-}
-
-#if AQ_LDS6
 // One slot's six fields from / to ONE LDS address (the slot's a, in bytes): three ds_read2st64_b64
 // / ds_write2st64_b64 at 0 / 50 / 100 / 150 / 200 / 250 x 512 B (LREC = 3200 slots of 8 B per
 // field). The pop waits for its own reads (lgkmcnt(0)) inside the asm -- the compiler cannot count
@@ -436,7 +423,12 @@ __device__ __forceinline__ void lds_push6(unsigned addr, double a, double b, dou
         : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb), "v"(dw)
         : "memory");
 }
-#endif
+// LDS byte address of ring index i of a wave's ring at byte offset ring8 (a multiple of WCAP * 8):
+// one shift-add and one and-or. vmask = (WCAP - 1) << 3 held in a VGPR (a gfx9 VOP3 reads one
+// scalar operand, so a literal mask and the scalar ring8 would split the and-or in two).
+__device__ __forceinline__ unsigned ring_addr(unsigned ring8, unsigned i, unsigned vmask) {
+    return ((i << 3) & vmask) | ring8;
+}
 // Ring slot of monotonic ring index i.
 __device__ __forceinline__ unsigned ring_slot(unsigned i) { return i % (unsigned)WCAP; }
 // Ring slot of b + k for a slot b < WCAP and k < WCAP: one mask (power-of-two ring) or one
@@ -455,14 +447,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
     // pair stores no midpoint: m = (a + b) / 2 is recomputed with the parent's own operands (:187),
     // bit-identical, so a pair is 44 B and a ring holds 256 pairs.
-#if AQ_LDS6
     __shared__ double s_pr[6 * LREC];
     const DtField s_dt{reinterpret_cast<unsigned*>(s_pr + 5 * LREC)};
-#else
-    __shared__ double s_pr[5 * LREC];
-    __shared__ unsigned s_dtw[LREC];
-    const DtField s_dt{s_dtw};
-#endif
     double* const s_a = s_pr;
     double* const s_b = s_pr + LREC;
     double* const s_fa = s_pr + 2 * LREC;
@@ -529,6 +515,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const unsigned main_jobs = tail_from * shares_main;
     const unsigned total_jobs = main_jobs + ((unsigned)P.nprob - tail_from) * shares_tail;
     const unsigned base = wid * WCAP;                            // this wave's ring
+    // its LDS byte offset (the pair block is the kernel's first LDS object, and a ring is WCAP * 8 B of
+    // each field: ring8 is a multiple of WCAP * 8, which ring_addr's and-or relies on)
+    const unsigned ring8 = pr_base + base * 8u;
+    __builtin_assume((ring8 & (unsigned)(WCAP * 8 - 1)) == 0u);
+    unsigned ring_vmask = (unsigned)((WCAP - 1) << 3);
+    asm volatile("" : "+v"(ring_vmask));   // kept in a VGPR (see ring_addr)
 
     Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u, 0u};
     // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
@@ -648,11 +640,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         const unsigned pb = S.pbot;
                         // a ring holds pairs of ONE integral (the rounds count without per-lane tags):
                         // take the leading run of pool pairs that share the first pair's integral
-                        ptag = (int)uni(s_dt[POOL0 + (pb & (PCAP - 1))] >> 8);
+                        ptag = (int)uni(s_dt[POOL0 + (pb & (PCAP - 1))] >> TAG_SHIFT);
                         for (unsigned q0 = 0; q0 < k; q0 += 64) {
                             const unsigned q = q0 + lane;
                             const unsigned long long bad =
-                                __ballot(q < k && (int)(s_dt[POOL0 + ((pb + q) & (PCAP - 1))] >> 8) != ptag);
+                                __ballot(q < k && (int)(s_dt[POOL0 + ((pb + q) & (PCAP - 1))] >> TAG_SHIFT) != ptag);
                             if (bad) {
                                 k = q0 + (unsigned)__builtin_ctzll(bad);
                                 break;
@@ -916,7 +908,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (alive) {
                     const unsigned j = base + mbcnt(am);
                     s_a[j] = l; s_b[j] = r; s_fa[j] = fl; s_fm[j] = fmid; s_fb[j] = fr;   // :192-197
-                    s_dt[j] = (unsigned)(D + 1) | ((unsigned)p << 8);
+                    const bool span = FID == F_COSH4 && cosh_main_span(l, r);
+                    s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }
                 bot = 0;
                 top = (unsigned)__popcll(am);
@@ -1198,29 +1191,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
             const bool act = lane < n;
             // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
-            const unsigned j0 = base + ring_wrap(b0s + lane);
-            const unsigned a0 = pr_base + j0 * 8u;
-#if AQ_LDS6
             double pa, pb, pfa, pfm, pfb;
             unsigned dt;
-            lds_pop6(a0, pa, pb, pfa, pfm, pfb, dt);
-#else
-            const lds_f64* pl = lds_at(a0);
-            const lds_f64* ph = lds_at(opaque(a0 + 3u * LREC * 8u));
-            const double pa = pl[0], pb = pl[LREC], pfa = pl[2 * LREC], pfm = ph[0], pfb = ph[LREC];
-            const unsigned dt = s_dt[j0];
-#endif
+            lds_pop6(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dt);
             const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
             const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
             Step2 st[2];
             // both midpoints lie in [pa, pb]: one range test for the pair
-            task_step_k<FID, 2>(tl, tr, tfl, tfr, eps2, tab, st, kk, FID == F_COSH4 ? (int)cosh_main_span(pa, pb) : -1);
+            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
+            // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
+            // compiler turns the byte test into an and plus a compare
+            unsigned long long nospan = 0ull;
+            if constexpr (FID == F_COSH4)
+                asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
+            // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
+            // measured 0.9 % slower)
+            const unsigned long long am = __ballot(act);
+            task_step_k<FID, 2>(tl, tr, tfl, tfr, eps2, tab, st, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
             // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
             // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
             // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
-            // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
-            // measured 0.9 % slower)
-            const unsigned long long am = __ballot(act), dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+            const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
             const unsigned long long okm = am & dm;
             // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
@@ -1236,7 +1227,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, dt, am);
             if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
                                     // takes and seeds switch the tag); checked in diagnostic builds
-                const int rtag = (int)(dt >> 8);
+                const int rtag = (int)(dt >> TAG_SHIFT);
                 b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
             }
             if (HIST) {
@@ -1254,30 +1245,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned cnt0 = (unsigned)__popcll(mask0);
             const unsigned cdt = dt + 1u;                       // depth + 1, same integral
             if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
-                const unsigned j = base + ring_wrap(__builtin_amdgcn_mbcnt_hi((unsigned)(mask0 >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((unsigned)mask0, b0s)));
-                const unsigned aj = pr_base + j * 8u;
-#if AQ_LDS6
-                lds_push6(aj, pa, pm, pfa, st[0].fmid, pfm, cdt);
-#else
-                lds_f64* ql = lds_at(aj);
-                lds_f64* qh = lds_at(opaque(aj + 3u * LREC * 8u));
-                ql[0] = pa; ql[LREC] = pm; ql[2 * LREC] = pfa; qh[0] = st[0].fmid; qh[LREC] = pfm;
-                s_dt[j] = cdt;
-#endif
+                lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, pm, pfa, st[0].fmid, pfm, cdt);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
-                const unsigned j = base + ring_wrap(__builtin_amdgcn_mbcnt_hi((unsigned)(mask1 >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((unsigned)mask1, b0s + cnt0)));
-                const unsigned aj = pr_base + j * 8u;
-#if AQ_LDS6
-                lds_push6(aj, pm, pb, pfm, st[1].fmid, pfb, cdt);
-#else
-                lds_f64* ql = lds_at(aj);
-                lds_f64* qh = lds_at(opaque(aj + 3u * LREC * 8u));
-                ql[0] = pm; ql[LREC] = pb; ql[2 * LREC] = pfm; qh[0] = st[1].fmid; qh[LREC] = pfb;
-                s_dt[j] = cdt;
-#endif
+                lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), pm, pb, pfm, st[1].fmid, pfb, cdt);
             }
             b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
             if constexpr (DIAG) {
