@@ -169,14 +169,16 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
     """A batch of integrals over every rank of `group`, rebalanced between launches (module doc).
 
     rebalance=False is the static partition for comparison: integral i's shard s always runs on rank
-    s mod world (the per-GPU subranges of the north star's first sentence)."""
+    s mod world (the per-GPU subranges of the north star's first sentence).
+
+    shards_per_integral=1 makes whole integrals the units (static: integral i on rank i mod world):
+    the choice for batches of small trees, whose shards would be seeding-bound."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     a = np.ascontiguousarray(a, np.float64)
     b = np.ascontiguousarray(b, np.float64)
     n = a.size
-    S = int(shards_per_integral or 4 * world)
-    S = max(world, S)
+    S = max(1, int(shards_per_integral or 4 * world))
     window = int(window or max(1, min(n, 8192 // S)))
     dev = torch.device("cpu") if dist.get_backend(group) != "nccl" else torch.device("cuda", runner.ctx.device)
     if runner is None:
@@ -201,7 +203,7 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
         if rebalance:
             plan = lpt_plan(np.array([shard_cost[s] for _, s in units]), world)
         else:
-            plan = [[u for u, (_, s) in enumerate(units) if s % world == r] for r in range(world)]
+            plan = [[u for u, (i, s) in enumerate(units) if (s if S > 1 else i) % world == r] for r in range(world)]
         loads = [sum(shard_cost[units[u][1]] for u in p) for p in plan]
         imb.append(max(loads) / (sum(loads) / world))
         mine = [units[u] for u in plan[rank]]

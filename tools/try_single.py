@@ -8,7 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from ppls_amd import Context, Problem  # noqa: E402
+from ppls_amd import Context, Problem, SIN_RECIP  # noqa: E402
 
 
 def main():
@@ -19,7 +19,8 @@ def main():
     ctx.set_level_histograms(False)
     out = {"lib": os.environ.get("AQ_LIB", "default")}
     for name, p in [("one_task", Problem(eps=1e9)), ("eps1e-3", Problem(eps=1e-3)), ("eps1e-6", Problem(eps=1e-6)),
-                    ("eps1e-8", Problem(eps=1e-8)), ("eps1e-10", Problem(eps=1e-10)), ("eps1e-12", Problem(eps=1e-12))]:
+                    ("eps1e-8", Problem(eps=1e-8)), ("eps1e-10", Problem(eps=1e-10)), ("eps1e-12", Problem(eps=1e-12)),
+                    ("sin_recip_eps1e-9", Problem(integrand=SIN_RECIP, a=1e-4, b=1.0, eps=1e-9))]:
         ctx.integrate_async(p, 0)
         ctx.synchronize()
         ctx.kernel_timing(True)
