@@ -123,11 +123,12 @@ def tasks_per_process(res: Result):
 
 # ---- the rebalanced batch ----------------------------------------------------------------------
 
-def lpt_plan(costs: np.ndarray, world: int) -> List[List[int]]:
+def lpt_plan(costs: np.ndarray, world: int, start=None) -> List[List[int]]:
     """Longest-processing-time-first assignment of units to ranks (deterministic: ties by index),
-    identical on every rank because every rank holds the same cost vector."""
+    identical on every rank because every rank holds the same cost vector. `start`: the ranks'
+    loads so far (the earlier rounds' measured tasks), so a round's odd unit goes where it evens out."""
     order = sorted(range(len(costs)), key=lambda u: (-float(costs[u]), u))
-    load = [0.0] * world
+    load = [0.0] * world if start is None else [float(x) for x in start]
     plan: List[List[int]] = [[] for _ in range(world)]
     for u in order:
         r = min(range(world), key=lambda k: (load[k], k))
@@ -178,7 +179,10 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
     a = np.ascontiguousarray(a, np.float64)
     b = np.ascontiguousarray(b, np.float64)
     n = a.size
-    S = max(1, int(shards_per_integral or 4 * world))
+    # default unit: the whole integral when the batch gives every rank several (shards of small trees
+    # are seeding-bound: config 4's 4096 sin(1/x) integrals over 8 ranks, makespan 0.75 ms whole vs
+    # 4.56 ms rebalanced in 32 shards each); else 4 shards per rank and integral
+    S = max(1, int(shards_per_integral or (1 if n >= 4 * world else 4 * world)))
     window = int(window or max(1, min(n, 8192 // S)))
     dev = torch.device("cpu") if dist.get_backend(group) != "nccl" else torch.device("cuda", runner.ctx.device)
     if runner is None:
@@ -188,6 +192,7 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
     seen = np.zeros(S)
     my_tasks = 0
     my_ms = 0.0
+    done = np.zeros(world)                # measured tasks each rank has run (the same on every rank)
     imb = []
     rounds = 0
     # the first round has no measurements (uniform costs): keep it short, so the unplanned part of
@@ -201,7 +206,7 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
         ids = np.arange(w0, w1)
         units = [(int(i), s) for i in ids for s in range(S)]
         if rebalance:
-            plan = lpt_plan(np.array([shard_cost[s] for _, s in units]), world)
+            plan = lpt_plan(np.array([shard_cost[s] for _, s in units]), world, start=done)
         else:
             plan = [[u for u, (i, s) in enumerate(units) if (s if S > 1 else i) % world == r] for r in range(world)]
         loads = [sum(shard_cost[units[u][1]] for u in p) for p in plan]
@@ -225,6 +230,8 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
         t = torch.from_numpy(full).to(dev)   # (`full` is this round's scratch: reduced in place is fine)
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         full = t.cpu().numpy()
+        for r in range(world):
+            done[r] += float(sum(full[u, XL] for u in plan[r]))
         for u, (i, s) in enumerate(units):
             total[i, :XL + 3] += full[u, :XL + 3]
             seen[s] += 1

@@ -122,7 +122,8 @@ class _OracleBatchRunner:
         return np.array(rows, np.int64).reshape(-1, 72)
 
 
-def _batch_worker(rank, world, port, rebalance, q):
+def _batch_worker(rank, world, port, rebalance, *rest):
+    shards, q = (rest[0], rest[1]) if len(rest) == 2 else (None, rest[0])   # (_run appends the queue)
     _init(rank, world, port)
     try:
         from ppls_amd.dist import integrate_batch_distributed
@@ -130,7 +131,7 @@ def _batch_worker(rank, world, port, rebalance, q):
         a = np.full(n, 1e-4)
         b = np.ones(n)
         r = integrate_batch_distributed(a, b, 1e-7, integrand=1, runner=_OracleBatchRunner(),
-                                        shards_per_integral=4 * world, window=3, rebalance=rebalance)
+                                        shards_per_integral=shards or 4 * world, window=3, rebalance=rebalance)
         q.put((rank, (r.area.tolist(), r.tasks.tolist(), r.accepted.tolist(), r.tasks_per_rank, r.rounds)))
     finally:
         dist.destroy_process_group()
@@ -152,4 +153,18 @@ def test_gloo_rebalanced_batch(oracle, rebalance):
         assert ratio < 1.15, per_rank
     else:
         assert ratio > 1.3, per_rank
+    assert results[1] == results[0]
+
+
+@pytest.mark.parametrize("rebalance", [False, True])
+def test_gloo_batch_whole_integral_units(oracle, rebalance):
+    """Whole integrals as the units (shards_per_integral=1, the default for batches of >= 4 integrals
+    per rank): exact counts, and 12 equal integrals split 6 / 6 over 2 ranks either way."""
+    world = 2
+    results = _run(_batch_worker, world, rebalance, 1, timeout=300)
+    want = oracle.integrate(oracle.SIN_RECIP, 1e-4, 1.0, 1e-7)
+    area, tasks, acc, per_rank, rounds = results[0]
+    assert all(t == want.tasks for t in tasks) and all(x == want.leaves for x in acc)
+    assert all(abs(v - want.area) <= 1e-12 * abs(want.area) for v in area)
+    assert per_rank == [6 * want.tasks, 6 * want.tasks]
     assert results[1] == results[0]
