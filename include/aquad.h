@@ -202,11 +202,12 @@ int aq_eval_cosh(aq_ctx *ctx, size_t n, const double *x, double *out);
  * stream; aq_kernel_time returns the summed milliseconds and launch count since the last reset. */
 int aq_kernel_timing(aq_ctx *ctx, int enable);
 int aq_kernel_time(aq_ctx *ctx, double *total_ms, uint64_t *launches);
-/* Per-workgroup timeline of the persistent kernel (40 uint64 words per workgroup: realtime stamps
- * at entry / seeded / first idle / exit in 100 MHz ticks, rounds, tasks, chunks and records moved
- * through the HBM queue, produce/idle ticks, seeds, max stack depth, CU slot, records received,
- * active lanes summed over rounds, shader-clock cycles per round phase and for seeding, then
- * records moved through the workgroup's HBM cellar).
+/* Per-workgroup timeline of the persistent kernel (48 uint64 words per workgroup: realtime stamps
+ * in 100 MHz ticks -- entry, init, first seed, seeded, last round, first idle, termination seen,
+ * loop exit, flushed, fold, exit -- rounds, tasks, chunks and records moved through the HBM queue,
+ * seeds, max ring size, CU slot, active lanes summed over rounds, shader-clock cycles per round
+ * phase and per seeding phase, records moved through the wave cellars; field names in
+ * ppls_amd.Context.DIAG_FIELDS).
  * Runs an instrumented kernel variant. aq_diagnostics returns the number of workgroup records. */
 int aq_set_diagnostics(aq_ctx *ctx, int enable);
 int aq_diagnostics(aq_ctx *ctx, uint64_t *out, int cap_words);

@@ -128,3 +128,15 @@ def test_exact_round_is_exported_host_code(lib):
 
 def test_user_integrand_name(lib):
     assert lib.aq_user_integrand_name().startswith(b"gauss")
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/conda/include/mpi.h"), reason="no MPI headers in this image")
+def test_integration_mpi_binding_compiles(tmp_path):
+    """INTEGRATION.md §1's C + MPI binding compiles (warnings as errors) against include/aquad.h, so
+    the documented boundary cannot drift from the header."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    src = re.search(r"```c\n(.*?)```", doc, re.S).group(1)
+    c = tmp_path / "aquadPartA_gpu.c"
+    c.write_text(src)
+    subprocess.run(["gcc", "-Wall", "-Wextra", "-Werror", "-c", "-I/opt/conda/include", "-I", os.path.join(ROOT, "include"),
+                    "-o", str(tmp_path / "b.o"), str(c)], check=True, capture_output=True, text=True, timeout=60)
