@@ -104,6 +104,8 @@ const char *aq_user_integrand_name(void);
  * launch: wavefronts expand sibling-pair frontiers in LDS (task body :183-202), accumulate accepted
  * areas, and rebalance through an HBM work queue (the bag of tasks, :152-165).
  * Bit-identical interval tree: `tasks` and `accepted` equal the reference's counts exactly.
+ * The synchronous calls (aq_integrate, aq_integrate_shard) use an internal result slot, never the
+ * caller's async slots, and read it back with one small kernel into pinned host memory.
  */
 int aq_integrate(aq_ctx *ctx, const aq_problem *p, aq_result *res);
 

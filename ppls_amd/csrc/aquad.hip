@@ -330,6 +330,35 @@ __global__ __launch_bounds__(128) void k_reset(Ctl* __restrict__ ctls, int first
     }
 }
 
+// The synchronous path's read-back (aq_integrate / aq_integrate_shard): one workgroup copies the
+// internal sync slot's result -- sums, exact limbs, the per-workgroup words of a per-CU launch, the
+// histograms when written -- straight into pinned host memory, then zeroes the slot for the next
+// call. One small launch in place of a reset kernel, a memset and three or four device-to-host
+// copies around every call.
+struct SyncOut {
+    SlotSums sums;
+    XSum area;
+    unsigned long long hist[2 * AQ_MAX_LEVELS];
+    unsigned long long parts[2 * MAXG];
+};
+__global__ __launch_bounds__(256) void k_fetch_sync(Ctl* __restrict__ c, unsigned long long* __restrict__ parts, int grid,
+                                                    int with_parts, int with_hist, SyncOut* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t == 0) out->sums = c->sums;
+    for (int i = t; i < XS_LIMBS; i += blockDim.x) out->area.limb[i] = c->area.limb[i];
+    if (with_hist)
+        for (int i = t; i < 2 * AQ_MAX_LEVELS; i += blockDim.x) out->hist[i] = c->hist[i];
+    if (with_parts)
+        for (int i = t; i < 2 * grid; i += blockDim.x) out->parts[i] = parts[i];
+    __syncthreads();   // every read precedes the zeroing
+    if (t == 0) c->sums = SlotSums{};
+    for (int i = t; i < XS_LIMBS; i += blockDim.x) c->area.limb[i] = 0;
+    if (with_hist)
+        for (int i = t; i < 2 * AQ_MAX_LEVELS; i += blockDim.x) c->hist[i] = 0ull;
+    if (with_parts)
+        for (int i = t; i < 2 * grid; i += blockDim.x) parts[i] = 0ull;
+}
+
 // aq_integrate_group: one rank's contribution to the RCCL exchange. sum_row (int64, summed over
 // ranks): limbs, tasks, accepted, spilled. info (gathered from every rank): tasks, levels, error,
 // then the rank's per-workgroup pack_cu words (grid of them; zero when not kept).
