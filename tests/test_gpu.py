@@ -209,6 +209,38 @@ def test_many_integrals_one_launch(ctx, oracle, trees):
         assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
 
 
+@pytest.mark.parametrize("k", [2, 11, 12, 15, 16])
+def test_few_integrals_static_jobs(ctx, oracle, trees, k):
+    """Launches of fewer than 16 integrals seed one share per wave with a static, rotated stride
+    (per-CU instance below 12 integrals, the bulk instance from 12 to 15); 16 claims jobs. Every
+    integral is its own exact tree; the cosh4 [0,5] ones match the golden counts."""
+    g = trees["cosh4_eps1e-8"]
+    a, b = oracle.batch_bounds(k)
+    a[0], b[0] = 0.0, 5.0
+    a[-1], b[-1] = 0.0, 5.0
+    ctx.integrate_many_async(a, b, 1e-8, first_slot=100)
+    for i in range(k):
+        r = ctx.fetch(100 + i)
+        o = oracle.integrate(a=a[i], b=b[i], eps=1e-8)
+        assert (r.tasks, r.accepted) == (o.tasks, o.leaves), (k, i)
+        assert abs(r.area - o.area) <= AREA_RTOL * abs(o.area)
+    for i in (0, k - 1):
+        assert (ctx.fetch(100 + i).tasks, ctx.fetch(100 + i).accepted) == (g["tasks"], g["leaves"])
+
+
+def test_sync_call_leaves_async_slots_alone(ctx, trees):
+    """aq_integrate runs in an internal slot: a pending async slot keeps its own result."""
+    from ppls_amd import Problem
+    g3, g10 = trees["cosh4_eps1e-3"], trees["cosh4_eps1e-10"]
+    ctx.integrate_async(Problem(eps=1e-3), 0)
+    r = ctx.integrate(Problem(eps=1e-10))
+    assert (r.tasks, r.accepted) == (g10["tasks"], g10["leaves"])
+    r0 = ctx.fetch(0)
+    assert (r0.tasks, r0.accepted) == (g3["tasks"], g3["leaves"])
+    r = ctx.integrate(Problem(eps=1e-3))      # the internal slot starts from zero again
+    assert (r.tasks, r.accepted) == (g3["tasks"], g3["leaves"])
+
+
 def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
     """MAXK integrals with random bounds in ONE persistent launch (the bench's launch shape); the
     first 256 against the committed golden fixture, all of them against the oracle."""
