@@ -2,30 +2,30 @@
 //
 // Reference: /root/reference/aquadPartA.c. The farmer's LIFO bag (:125-173) and the workers' task
 // body (:183-202) become one persistent launch:
-//   * the unit of work is a SIBLING PAIR {a, b, F(a), F(m), F(b), depth | integral<<8}
-//     = the two tasks [a,m] and [m,b] a refining parent pushes (:192-197); m = (a+b)/2 is recomputed
-//     from the parent's own operands (:187), so it is not stored. A pair is 44 bytes for two tasks
-//     (two separate records would be 72), and it hands every lane two independent evaluations: the
-//     K=2 cosh chains interleave (aq_libm.h cosh_main_k).
+//   * the unit of work is a SIBLING PAIR {a, b, F(a), F(m), F(b), dt} = the two tasks [a,m] and [m,b]
+//     a refining parent pushes (:192-197); m = (a+b)/2 is recomputed from the parent's own operands
+//     (:187), so it is not stored; dt = depth | SPAN_BIT | integral << 16. A pair is six 8-byte LDS
+//     fields for two tasks, and it hands every lane two independent evaluations: the K=2 cosh chains
+//     interleave (aq_libm.h cosh_main_k).
 //   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of pairs. A round pops
 //     <= 64 pairs, evaluates F at both midpoints in FP64 (glibc-exact cosh), applies the reference's
 //     refine test (:191) to both tasks and pushes each refining task's children as a new pair, with a
-//     ballot / mbcnt compaction: no workgroup barrier, no HBM traffic.
-//   * ring overflow goes to the wave's private HBM cellar (no lock; refilled when the ring runs dry);
-//     a locked LDS pool feeds idle sibling waves; an HBM ticket queue of pair chunks moves work
-//     across CUs (what the bag of tasks is for), driven by one elected leader wave per idle
-//     workgroup; busy waves donate to waiting tickets.
+//     ballot / mbcnt compaction: no workgroup barrier, no HBM traffic. Rounds run in bursts with
+//     all ring state wave-uniform (SGPRs).
+//   * ring overflow goes to the wave's private HBM cellar (no lock; prefetched back when the ring
+//     runs low); a locked LDS pool feeds idle sibling waves; an HBM ticket queue of pair chunks moves
+//     work across CUs (what the bag of tasks is for), driven by one elected leader wave per idle
+//     workgroup; busy waves donate to waiting tickets. Termination: a two-level token count (QCtl).
 //   * jobs: job j seeds share j % shares of integral j / shares. Seeding is WAVE-LOCAL: virtual
 //     worker vw = share*nshards + shard of V owns the depth-D positions j = k*V + (k odd ? V-1-vw : vw)
 //     (snake order). All F evaluations of the positions' paths (depths 0..D) are independent (pure
 //     (l+r)/2 recursion), so one wave evaluates them in one pass, decides every node, and keeps the
 //     children of each surviving position node as its first pair. A task at depth <= D is counted by
 //     the owner of its leftmost descendant position (the partition oracle/aq_oracle.c restates).
-//     Wave w seeds job w first; later jobs are claimed from a counter (one claim in flight per wave),
-//     so the tail of one integral overlaps the start of the next, and waves that draw light shares
-//     take more of them.
+//     Launches of many integrals claim jobs from a counter (one claim in flight per wave), so the
+//     tail of one integral overlaps the start of the next; launches of few take a static stride.
 //   * accepted areas / task counts accumulate per lane in registers per integral and are flushed
-//     (wave reduction + a few device atomics into the integral's slot: counts, and the area into an
+//     (DPP wave reduction + device atomics into the integral's slot: counts, and the area into an
 //     exact fixed-point accumulator, aq_xsum.h) when a wave switches integral or exits (the
 //     farmer's `result += buff[0]`, :149).
 // Every decision is the reference's own arithmetic on the same operands, so the interval tree --
