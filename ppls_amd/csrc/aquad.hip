@@ -43,7 +43,7 @@
 namespace aq {
 
 // ------------------------------------------------------------------------------------------------
-// Device result block (one per async slot), zeroed before each call.
+// Result block of the level-synchronous path (aq_integrate_levels), zeroed before each call.
 // ------------------------------------------------------------------------------------------------
 struct DevResults {
     double area;
@@ -52,10 +52,6 @@ struct DevResults {
     unsigned long long spilled;
     unsigned int levels;
     unsigned int error;        // AQ_E* as positive bit flags (see err_bit)
-    unsigned int q_tail;       // chunk slots claimed by producers
-    unsigned int q_head;       // tickets taken by idle workgroups
-    int q_tokens;              // busy workgroups + records in published, unconsumed chunks
-    unsigned int pad[3];
     unsigned long long tasks_per_level[AQ_MAX_LEVELS];
     unsigned long long leaves_per_level[AQ_MAX_LEVELS];
     unsigned long long cu_tasks[AQ_CU_SLOTS];
