@@ -26,7 +26,19 @@
 
 namespace aq {
 
-struct ExpEntry {  // tab[2k], tab[2k+1] of glibc's __exp_data.tab
+// glibc's __exp_data.tab[2j], tab[2j+1] as the device's global copy holds them.
+struct ExpPair {
+    uint64_t tail_bits;
+    uint64_t sbits;
+};
+
+// One entry of the LDS copy (stage_exp_table): the same pair, 16-B aligned for one ds_read_b128.
+// (r02 A/B, tools/ab.sh: a 32-B entry that also carried 2^(-j/128)'s high word, so that cosh's first
+// reciprocal estimate u (1 - tmp) replaced v_rcp_f64 -- exact on 3.4e10 points, but 2 FMAs, 2 integer
+// ops and 2 LDS reads more per round -- measured 1.0 % slower: v_rcp_f64, ~3x an FMA's issue cost
+// alone (tools/ubench_issue.hip), overlaps the surrounding VALU work. A 256-entry copy indexed by ki's
+// low byte through one SDWA shift (2 integer ops fewer per round) read as ds_read2_b64: 0.8 % slower.)
+struct alignas(16) ExpEntry {
     uint64_t tail_bits;
     uint64_t sbits;
 };
@@ -383,8 +395,11 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
 }
 
 // Stage the exp table into LDS (call from every thread, then __syncthreads()).
-__device__ __forceinline__ void stage_exp_table(ExpEntry* lds, const ExpEntry* __restrict__ g) {
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) lds[i] = g[i];
+__device__ __forceinline__ void stage_exp_table(ExpEntry* lds, const ExpPair* __restrict__ g) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+        lds[i].tail_bits = g[i].tail_bits;
+        lds[i].sbits = g[i].sbits;
+    }
 }
 
 }  // namespace aq

@@ -253,7 +253,7 @@ struct StreamParams {
     Chunk* chunks;
     Cellar* cellar;                 // [gridDim.x * NW]
     unsigned* ready;
-    const ExpEntry* gtab;
+    const ExpPair* gtab;
     LaunchHint* hint;
     int per_cu;                     // also keep per-workgroup partials (per-CU task counts; lone integrals)
     int static_jobs;                // fewer than STATIC_MAXK integrals: static job stride (see k_stream)

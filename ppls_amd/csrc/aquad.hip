@@ -63,12 +63,24 @@ struct DevResults {
 // ------------------------------------------------------------------------------------------------
 template <int FID, bool COSH_ONLY>
 __global__ __launch_bounds__(256) void k_eval(const double* __restrict__ x, double* __restrict__ out, size_t n,
-                                              const ExpEntry* __restrict__ gtab) {
+                                              const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[128];
     stage_exp_table(tab, gtab);
     __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        out[i] = COSH_ONLY ? cosh_glibc(x[i], tab) : integrand<FID>(x[i], tab);
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    if constexpr (FID == F_COSH4 && !COSH_ONLY) {
+        // F through the persistent kernels' batched path (integrand_k: two interleaved cosh chains,
+        // the table reciprocal estimate), two points per lane; aq_eval_cosh keeps the scalar one
+        const ExpConsts kk = pinned_exp_consts();
+        for (size_t i = 2 * gid; i < n; i += 2 * stride) {
+            const double xx[2] = {x[i], x[i + 1 < n ? i + 1 : i]};
+            double ff[2];
+            integrand_k<F_COSH4, 2>(xx, ff, tab, kk);
+            out[i] = ff[0];
+            if (i + 1 < n) out[i + 1] = ff[1];
+        }
+    } else {
+        for (size_t i = gid; i < n; i += stride) out[i] = COSH_ONLY ? cosh_glibc(x[i], tab) : integrand<FID>(x[i], tab);
     }
 }
 
@@ -80,7 +92,7 @@ struct Rec {
 };
 
 template <int FID>
-__global__ __launch_bounds__(64) void k_root(double a, double b, Rec* out, const ExpEntry* __restrict__ gtab) {
+__global__ __launch_bounds__(64) void k_root(double a, double b, Rec* out, const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[128];
     stage_exp_table(tab, gtab);
     __syncthreads();
@@ -98,7 +110,7 @@ template <int FID>
 __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
                                                unsigned* __restrict__ n_out, unsigned cap_out, double eps, int depth,
                                                int max_depth, DevResults* __restrict__ res,
-                                               const ExpEntry* __restrict__ gtab) {
+                                               const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[128];
     __shared__ double s_area[4];
     __shared__ unsigned s_cnt[2][4];
@@ -186,7 +198,7 @@ template <int FID>
 __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
                                                     unsigned* __restrict__ n_out, unsigned cap_out, double eps,
                                                     int depth, int max_depth, LevelPart* __restrict__ parts,
-                                                    const ExpEntry* __restrict__ gtab) {
+                                                    const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[128];
     __shared__ double s_h[4], s_l[4];
     __shared__ unsigned s_t[4], s_a[4], s_e[4];
@@ -270,7 +282,7 @@ __global__ __launch_bounds__(64) void k_level_fold(const LevelPart* __restrict__
 }
 
 template <int FID>
-__global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* out, const ExpEntry* __restrict__ gtab) {
+__global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* out, const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[128];
     stage_exp_table(tab, gtab);
     __syncthreads();

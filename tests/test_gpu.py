@@ -72,6 +72,22 @@ def test_device_integrand_bit_exact(ctx, oracle):
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
+def test_device_batched_integrand_bit_exact(ctx, oracle, libm_bits):
+    """F through the persistent kernels' batched path (aq_eval_integrand: integrand_k, two points per
+    lane, the table reciprocal estimate in cosh's 0.5/t) against the restated glibc cosh^4, on the
+    committed libm fixture points and 8 M random points: the main range, both sides of its ends, and
+    lanes whose two points fall on different paths."""
+    rng = np.random.default_rng(14)
+    x = np.concatenate([libm_bits["x"].view(np.float64), rng.uniform(0.0, 5.0, 4_000_000),
+                        rng.uniform(0.3, 0.4, 1_000_000), rng.uniform(21.5, 22.5, 1_000_000),
+                        rng.uniform(-30.0, 30.0, 2_000_000)])
+    c = oracle.cosh(x)
+    want = ((c * c) * c) * c          # the reference macro's ((c*c)*c)*c (aquadPartA.c:46)
+    got = ctx.eval_integrand(x)
+    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, [(float(x[i]), float(got[i]), float(want[i])) for i in bad[:10]]
+
+
 def test_device_sin_recip_faithful(ctx, oracle):
     rng = np.random.default_rng(13)
     x = rng.uniform(1e-4, 1.0, 20000)

@@ -25,7 +25,7 @@
     } while (0)
 
 template <int ILP, int MODE>
-__global__ void k_ubench(const aq::ExpEntry* __restrict__ gtab, double* out, int iters, double x0, double dx) {
+__global__ void k_ubench(const aq::ExpPair* __restrict__ gtab, double* out, int iters, double x0, double dx) {
     __shared__ aq::ExpEntry tab[128];
     aq::stage_exp_table(tab, gtab);
     __syncthreads();
@@ -54,7 +54,7 @@ __global__ void k_ubench(const aq::ExpEntry* __restrict__ gtab, double* out, int
 }
 
 template <int ILP, int MODE>
-int run(const char* name, aq::ExpEntry* dtab, double* dout, int cus, int block, int blocks_per_cu, int iters) {
+int run(const char* name, aq::ExpPair* dtab, double* dout, int cus, int block, int blocks_per_cu, int iters) {
     const int grid = cus * blocks_per_cu;
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
@@ -78,10 +78,10 @@ int main() {
     hipDeviceProp_t p;
     CHECK(hipGetDeviceProperties(&p, 0));
     const int cus = p.multiProcessorCount;
-    aq::ExpEntry* dtab;
+    aq::ExpPair* dtab;
     double* dout;
-    CHECK(hipMalloc(&dtab, sizeof(aq::ExpEntry) * 128));
-    CHECK(hipMemcpy(dtab, aq_exp_tab_host, sizeof(aq::ExpEntry) * 128, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&dtab, sizeof(aq::ExpPair) * 128));
+    CHECK(hipMemcpy(dtab, aq_exp_tab_host, sizeof(aq::ExpPair) * 128, hipMemcpyHostToDevice));
     CHECK(hipMalloc(&dout, sizeof(double) * (size_t)cus * 2048 * 4));
     const int it = 2000;
     for (int bpc : {1, 2, 4, 8}) run<1, 0>("F=cosh^4", dtab, dout, cus, 256, bpc, it);

@@ -41,7 +41,7 @@ struct Counts {
     double relerr_y0, relerr_y1;
 };
 
-__global__ void k_recip(const aq::ExpEntry* __restrict__ gtab, Counts* out, int iters, int pass, uint64_t seed) {
+__global__ void k_recip(const aq::ExpPair* __restrict__ gtab, Counts* out, int iters, int pass, uint64_t seed) {
     __shared__ aq::ExpEntry tab[128];
     aq::stage_exp_table(tab, gtab);
     __syncthreads();
@@ -49,6 +49,22 @@ __global__ void k_recip(const aq::ExpEntry* __restrict__ gtab, Counts* out, int 
     Counts c = {0, 0, 0, 0, 0, 0.0, 0.0};
     for (int it = 0; it < iters; ++it) {
         const uint64_t z = mix64(seed + (gid * (uint64_t)iters + it) * 0x9E3779B97F4A7C15ull);
+        if (pass == 2) {
+            // the batched path itself: cosh_main_k on two points (table reciprocal estimate when
+            // AQ_TAB_RECIP) against RN(0.5 t + RN(0.5 / t)) with the compiler's IEEE division
+            double xs[2], cm[2];
+            for (int k = 0; k < 2; ++k) {
+                const uint64_t zk = mix64(z + k);
+                xs[k] = 0.34657359027997264 + (double)(zk >> 11) * 0x1p-53 * (22.0 - 0.34657359027997264);
+            }
+            aq::cosh_main_k<2, false>(xs, cm, tab, aq::pinned_exp_consts());
+            for (int k = 0; k < 2; ++k) {
+                const double tk = aq::exp_glibc(xs[k], tab);
+                c.n += 1;
+                c.bad3 += (cm[k] != __fma_rn(tk, 0.5, 0.5 / tk));
+            }
+            continue;
+        }
         double t;
         if (pass == 0) {
             const double u = (double)(z >> 11) * 0x1p-53;
@@ -83,14 +99,15 @@ int main(int argc, char** argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 256;
     const int threads = 256;
     const size_t nt = (size_t)blocks * threads;
-    aq::ExpEntry* dtab;
+    aq::ExpPair* dtab;
     Counts* dout;
-    CHECK(hipMalloc(&dtab, sizeof(aq::ExpEntry) * 128));
-    CHECK(hipMemcpy(dtab, aq_exp_tab_host, sizeof(aq::ExpEntry) * 128, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&dtab, sizeof(aq::ExpPair) * 128));
+    CHECK(hipMemcpy(dtab, aq_exp_tab_host, sizeof(aq::ExpPair) * 128, hipMemcpyHostToDevice));
     CHECK(hipMalloc(&dout, nt * sizeof(Counts)));
     std::vector<Counts> h(nt);
-    for (int pass = 0; pass < 2; ++pass) {
-        k_recip<<<blocks, threads>>>(dtab, dout, iters, pass, 0x1234567ull + pass);
+    const int reps2 = argc > 3 ? atoi(argv[3]) : 1;   // launches of pass 2 (the batched cosh path)
+    for (int pass = 0; pass < 2 + reps2; ++pass) {
+        k_recip<<<blocks, threads>>>(dtab, dout, iters, pass < 2 ? pass : 2, 0x1234567ull + pass);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(h.data(), dout, nt * sizeof(Counts), hipMemcpyDeviceToHost));
@@ -103,6 +120,11 @@ int main(int argc, char** argv) {
             s.bad3 += c.bad3;
             s.relerr_y0 = std::fmax(s.relerr_y0, c.relerr_y0);
             s.relerr_y1 = std::fmax(s.relerr_y1, c.relerr_y1);
+        }
+        if (pass >= 2) {
+            printf("{\"pass\": 2, \"seed\": %d, \"cosh_main_k_samples\": %llu, \"cosh_main_k_mismatch\": %llu}\n", pass,
+                   s.n, s.bad3);
+            continue;
         }
         printf("{\"pass\": %d, \"samples\": %llu, \"mismatch_newton0\": %llu, \"mismatch_newton1\": %llu, "
                "\"mismatch_newton2\": %llu, \"mismatch_second_order\": %llu, \"max_relerr_rcp_ulp53\": %.6g, \"max_relerr_newton1_ulp53\": %.6g}\n",
