@@ -270,7 +270,13 @@ __device__ __forceinline__ bool cosh_main_range(double x) {
 // one multiply (q = 0.5 y) fewer per evaluation, bit for bit the same value. The doubled scale costs
 // nothing: with Shift + 128 in place of Shift, ki grows by 128 (index ki & 127 unchanged; the
 // subtraction kd - Shift unchanged) and (ki << 13) adds exactly 2^20 to the scale's high word.
-template <int K, bool CHECK = true>
+//
+// TWICE: c[k] = 2 cosh(x[k]) = RN(t + y3), exactly twice glibc's value. With q = 0.5 y2 (exact) the
+// quotient correction's residual fma(-t, q, 0.5) is half the Newton residual e = fma(-t, y2, 1), so
+// RN(0.5 / t) = RN(q + r y2) = 0.5 RN(y2 + e y2) = 0.5 y3 (the next Newton iterate), and cosh =
+// RN(0.5 t + 0.5 y3) = 0.5 RN(t + y3): every halving is exact in this range. One multiply fewer per
+// evaluation and a shorter chain (e, y3, t + y3 against q, r, h, c).
+template <int K, bool CHECK = true, bool TWICE = false>
 __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab,
                                             const ExpConsts& kk) {
     double ax[K], kd[K], r[K], r2[K], tmp[K], t[K];
@@ -334,6 +340,15 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
             y[k] = __fma_rn(y[k], __fma_rn(e, e, e), y[k]);
         }
     }
+    if constexpr (TWICE) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const double e = __fma_rn(-t[k], y[k], 1.0);
+            c[k] = t[k] + __fma_rn(y[k], e, y[k]);                    // RN(t + y3) = 2 cosh
+        }
+        (void)q;
+        return out;
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         q[k] = 0.5 * y[k];
@@ -353,31 +368,35 @@ __device__ __forceinline__ bool cosh_main_span(double lo, double hi) {
     // compares, no subtracts.
     return ((int)hi_word(lo) >= 0x3fd62e43) && ((int)hi_word(hi) < 0x40360000);
 }
-template <int FID, int K>
+//
+// SCALED (cosh^4 only): f[k] = 16 F(x[k]), exactly, as ((s*s)*s)*s with s = 2 cosh (cosh_main_k
+// TWICE): every product is the reference's scaled by a power of two (f_scale<FID>(), aq_device.h).
+template <int FID, int K, bool SCALED = false>
 __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab,
                                             const ExpConsts& kk = ExpConsts{}, int range_hint = -1,
                                             unsigned long long out_mask = 0ull) {
     if constexpr (FID == F_COSH4) {
+        constexpr double cs = SCALED ? 2.0 : 1.0;   // c[k] holds cs * cosh
         double c[K];
         bool out;
         if (range_hint == 2) {
-            cosh_main_k<K, false>(x, c, tab, kk);
+            cosh_main_k<K, false, SCALED>(x, c, tab, kk);
             if (__builtin_expect(out_mask != 0ull, 0)) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
-                    if (!cosh_main_range(x[k])) c[k] = cosh_glibc(x[k], tab);
+                    if (!cosh_main_range(x[k])) c[k] = cs * cosh_glibc(x[k], tab);
             }
             out = false;
         } else if (range_hint >= 0) {
-            cosh_main_k<K, false>(x, c, tab, kk);
+            cosh_main_k<K, false, SCALED>(x, c, tab, kk);
             out = range_hint == 0;
         } else {
-            out = cosh_main_k<K>(x, c, tab, kk);
+            out = cosh_main_k<K, true, SCALED>(x, c, tab, kk);
         }
         if (__builtin_expect(__ballot(out) != 0ull, 0)) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (!cosh_main_range(x[k])) c[k] = cosh_glibc(x[k], tab);
+                if (!cosh_main_range(x[k])) c[k] = cs * cosh_glibc(x[k], tab);
         }
 #pragma unroll
         for (int k = 0; k < K; ++k) f[k] = c[k] * c[k];           // ((c*c)*c)*c, stage by stage so

@@ -487,7 +487,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if constexpr (DIAG) { if (tid == 0) s_dg[DG_T_INIT] = rtc(); }
 
     const double eps = P.eps;
-    const double eps2 = doubled_areas<FID>() ? 2.0 * eps : eps;   // the rounds compare doubled areas (task_step_k)
+    const double eps2 = eps / area_scale<FID>();   // the rounds compare doubled areas of f_scale F (task_step_k)
     const int max_depth = P.max_depth;
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
     unsigned shares_main = (unsigned)P.shares;
@@ -907,7 +907,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned long long am = __ballot(alive);
                 if (alive) {
                     const unsigned j = base + mbcnt(am);
-                    s_a[j] = l; s_b[j] = r; s_fa[j] = fl; s_fm[j] = fmid; s_fb[j] = fr;   // :192-197
+                    constexpr double fs = f_scale<FID>();   // the rounds' F values (exact scaling)
+                    s_a[j] = l; s_b[j] = r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
                     const bool span = FID == F_COSH4 && cosh_main_span(l, r);
                     s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }

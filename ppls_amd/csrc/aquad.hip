@@ -69,15 +69,15 @@ __global__ __launch_bounds__(256) void k_eval(const double* __restrict__ x, doub
     __syncthreads();
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
     if constexpr (FID == F_COSH4 && !COSH_ONLY) {
-        // F through the persistent kernels' batched path (integrand_k: two interleaved cosh chains,
-        // the table reciprocal estimate), two points per lane; aq_eval_cosh keeps the scalar one
+        // F through the persistent kernel's batched path (integrand_k: two interleaved cosh chains,
+        // 2 cosh and 16 F), two points per lane; aq_eval_cosh keeps the scalar one
         const ExpConsts kk = pinned_exp_consts();
         for (size_t i = 2 * gid; i < n; i += 2 * stride) {
             const double xx[2] = {x[i], x[i + 1 < n ? i + 1 : i]};
             double ff[2];
-            integrand_k<F_COSH4, 2>(xx, ff, tab, kk);
-            out[i] = ff[0];
-            if (i + 1 < n) out[i + 1] = ff[1];
+            integrand_k<F_COSH4, 2, true>(xx, ff, tab, kk);   // 16 F, as k_stream's rounds (exact /16)
+            out[i] = ff[0] / f_scale<F_COSH4>();
+            if (i + 1 < n) out[i + 1] = ff[1] / f_scale<F_COSH4>();
         }
     } else {
         for (size_t i = gid; i < n; i += stride) out[i] = COSH_ONLY ? cosh_glibc(x[i], tab) : integrand<FID>(x[i], tab);
