@@ -26,7 +26,8 @@ extern "C" {
 #endif
 
 #define AQ_OK 0
-#define AQ_EINVAL (-1)     /* bad argument (non-finite bounds, b < a, eps < 0, bad shard, outside the integrand's domain) */
+#define AQ_EINVAL (-1)     /* bad argument (non-finite bounds, b < a, eps < 0, bad shard, outside the integrand's domain;
+                            every integrand: each bound 0 or 2^-900 <= |x| <= 2^900) */
 #define AQ_EHIP (-2)       /* a HIP runtime call failed */
 #define AQ_ETIMEOUT (-3)   /* an on-device wait saw no progress for the stall bound (aq_set_stall_timeout) */
 #define AQ_EOVERFLOW (-4)  /* a frontier / work-queue capacity was exceeded */

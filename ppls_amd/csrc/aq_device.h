@@ -147,6 +147,54 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
     }
 }
 
+// Both tasks of a sibling pair [a, m], [m, b] (m = (a + b) / 2, the parent's midpoint) from the pair's
+// HALVED endpoints ha = a / 2, hb = b / 2, as k_stream's rings store them. With a = 2 ha exactly
+// (the validated domain keeps every coordinate's half normal, aq_abi.inc bounds_ok):
+//   m    = RN((a + b) / 2) = RN(ha + hb)               hm = m / 2 (exact)
+//   midL = RN((a + m) / 2) = RN(ha + hm)               midR = RN(hm + hb)             (:187)
+//   m - a = RN(m - 2 ha) = fma(ha, -2, m)              b - m = fma(hb, 2, -m), and alike for
+// the widths of :189 / :190 -- the reference's values, one operation each, so the three midpoints
+// cost three adds and one multiply where (l + r) / 2 costs an add and a multiply each. The
+// children pairs are {ha, hm} and {hm, hb}: already at hand. Returns m and hm for the pushes.
+template <int FID>
+__device__ __forceinline__ void pair_step_halves(double ha, double hb, double fa, double fm, double fb, double eps2,
+                                                 const ExpEntry* __restrict__ tab, Step2 (&s)[2], double& m,
+                                                 double& hm, const ExpConsts& kk, int range_hint,
+                                                 unsigned long long out_mask) {
+    m = ha + hb;                                             // the parent's midpoint (:187)
+    hm = 0.5 * m;
+    const double mid[2] = {ha + hm, hm + hb};                // :187 for [a, m] and [m, b]
+    const double fl[2] = {fa, fm}, fr[2] = {fm, fb};
+    // the parts that do not need F(mid) first (as task_step_k's AQ_EARLY_STEP)
+    double lr2e[2], wl[2], wr[2];
+    lr2e[0] = (fa + fm) * __fma_rn(ha, -2.0, m);             // (fl + fr) * (r - l), :185
+    lr2e[1] = (fm + fb) * __fma_rn(hb, 2.0, -m);
+    wl[0] = __fma_rn(ha, -2.0, mid[0]);                      // mid - l
+    wl[1] = mid[1] - m;
+    wr[0] = m - mid[0];                                      // r - mid
+    wr[1] = __fma_rn(hb, 2.0, -mid[1]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) asm volatile("" : "+v"(lr2e[k]), "+v"(wl[k]), "+v"(wr[k]));
+    double fmid[2];
+    integrand_k<FID, 2, (f_scale<FID>() != 1.0)>(mid, fmid, tab, kk, range_hint, out_mask);   // :188
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        s[k].fmid = fmid[k];
+        if constexpr (doubled_areas<FID>()) {
+            const double l2 = (fl[k] + fmid[k]) * wl[k];     // 2 * larea, :189
+            const double r2 = (fmid[k] + fr[k]) * wr[k];     // 2 * rarea, :190
+            s[k].area2 = l2 + r2;
+            s[k].refine = fabs(s[k].area2 - lr2e[k]) > eps2;   // :191 (strict >)
+        } else {
+            const double lrarea = lr2e[k] / 2;                // :185
+            const double larea = (fl[k] + fmid[k]) * wl[k] / 2;   // :189
+            const double rarea = (fmid[k] + fr[k]) * wr[k] / 2;   // :190
+            s[k].area2 = larea + rarea;                       // :199
+            s[k].refine = fabs((larea + rarea) - lrarea) > eps2;   // :191
+        }
+    }
+}
+
 // Double-double (hi + lo) sums of the accepted areas: every leaf area enters a per-lane pair
 // exactly (Knuth's TwoSum, six flops), the pairs reduce across the wave and the workers without
 // rounding, and only the final hi + lo is rounded -- so the area is the correctly rounded sum of

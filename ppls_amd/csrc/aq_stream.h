@@ -908,7 +908,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (alive) {
                     const unsigned j = base + mbcnt(am);
                     constexpr double fs = f_scale<FID>();   // the rounds' F values (exact scaling)
-                    s_a[j] = l; s_b[j] = r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
+                    // a pair holds its endpoints halved (aq_device.h pair_step_halves; exact)
+                    s_a[j] = 0.5 * l; s_b[j] = 0.5 * r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
                     const bool span = FID == F_COSH4 && cosh_main_span(l, r);
                     s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }
@@ -1195,8 +1196,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             double pa, pb, pfa, pfm, pfb;
             unsigned dt;
             lds_pop6(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dt);
-            const double pm = (pa + pb) / 2;                    // the parent's midpoint, recomputed (:187)
-            const double tl[2] = {pa, pm}, tr[2] = {pm, pb}, tfl[2] = {pfa, pfm}, tfr[2] = {pfm, pfb};
             Step2 st[2];
             // both midpoints lie in [pa, pb]: one range test for the pair
             // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
@@ -1208,7 +1207,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
             // measured 0.9 % slower)
             const unsigned long long am = __ballot(act);
-            task_step_k<FID, 2>(tl, tr, tfl, tfr, eps2, tab, st, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+            // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
+            double pm, hm;
+            pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
             // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
             // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
             // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
@@ -1246,10 +1247,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned cnt0 = (unsigned)__popcll(mask0);
             const unsigned cdt = dt + 1u;                       // depth + 1, same integral
             if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
-                lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, pm, pfa, st[0].fmid, pfm, cdt);
+                lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
-                lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), pm, pb, pfm, st[1].fmid, pfb, cdt);
+                lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
             }
             b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
             if constexpr (DIAG) {

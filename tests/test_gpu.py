@@ -73,8 +73,8 @@ def test_device_integrand_bit_exact(ctx, oracle):
 
 
 def test_device_batched_integrand_bit_exact(ctx, oracle, libm_bits):
-    """F through the persistent kernels' batched path (aq_eval_integrand: integrand_k, two points per
-    lane, the table reciprocal estimate in cosh's 0.5/t) against the restated glibc cosh^4, on the
+    """F through the persistent kernel's batched path (aq_eval_integrand: integrand_k, two points per
+    lane, computed as 16 F from 2 cosh as the rounds do, /16 exact) against the restated glibc cosh^4, on the
     committed libm fixture points and 8 M random points: the main range, both sides of its ends, and
     lanes whose two points fall on different paths."""
     rng = np.random.default_rng(14)
@@ -186,6 +186,11 @@ def test_errors(ctx):
         ctx.integrate(Problem(eps=float("nan")))
     with pytest.raises(AquadError, match="depth"):
         ctx.integrate(Problem(eps=1e-10, max_depth=10))
+    # the domain (include/aquad.h AQ_EINVAL): bounds 0 or 2^-900 <= |x| <= 2^900, |x| <= 170 for cosh^4
+    for a, b, f in [(1e-300, 1.0, 1), (0.0, 2.0 ** 901, 1), (0.0, 171.0, 0)]:
+        with pytest.raises(AquadError):
+            ctx.integrate(Problem(a=a, b=b, eps=1e-3, integrand=f))
+    assert ctx.integrate(Problem(a=2.0 ** -900, b=1.0, eps=1e-3, integrand=1)).tasks > 0
     # the context is still usable after an error
     assert ctx.integrate(Problem(eps=1e-3)).tasks == 6567
 
