@@ -121,6 +121,11 @@ constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetche
 #define AQ_PREFETCH 1
 #endif
 constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch (13 VGPRs)
+#ifndef AQ_SPILL
+#define AQ_SPILL 64   // r02 A/B: 128 at once 4.0 % slower at eps 1e-10, 6.5 % at 1e-12 (more refills)
+#endif
+constexpr int SPILL = AQ_SPILL;   // pairs a ring above WCAP - 64 moves to its cellar at once (a multiple of 64)
+static_assert(SPILL % 64 == 0 && SPILL <= WCAP - 128, "spill whole lanes' worth, keep 64 pairs in the ring");
 
 struct alignas(128) Line {
     unsigned v;
@@ -1036,13 +1041,16 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // ---- keep the ring from overflowing: its bottom 64 pairs go to the cellar, else the pool,
         //      else an HBM chunk
         if (size > (unsigned)(WCAP - 64)) {
-            if (ctop + 64u <= (unsigned)CCAP) {
-                const unsigned i = ctop + lane, j = base + ring_slot(bot + lane);
-                cel->a[i] = s_a[j]; cel->b[i] = s_b[j];
-                cel->fa[i] = s_fa[j]; cel->fm[i] = s_fm[j]; cel->fb[i] = s_fb[j]; cel->dt[i] = s_dt[j];
-                ctop += 64u;
-                bot += 64u;
-                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], 64ull); }
+            if (ctop + (unsigned)SPILL <= (unsigned)CCAP) {
+#pragma unroll
+                for (unsigned q = 0; q < (unsigned)SPILL; q += 64u) {
+                    const unsigned i = ctop + q + lane, j = base + ring_slot(bot + q + lane);
+                    cel->a[i] = s_a[j]; cel->b[i] = s_b[j];
+                    cel->fa[i] = s_fa[j]; cel->fm[i] = s_fm[j]; cel->fb[i] = s_fb[j]; cel->dt[i] = s_dt[j];
+                }
+                ctop += (unsigned)SPILL;
+                bot += (unsigned)SPILL;
+                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
