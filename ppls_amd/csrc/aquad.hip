@@ -194,63 +194,97 @@ struct LevelPart {
     double hi, lo, tasks, leaves, err, levels, pad0, pad1;
 };
 
+// Children are appended with ONE atomic per workgroup and chunk of LEVEL_R x 256 records: a wave-level
+// atomic per 64 records had made the wide levels a serial fan-in on the one counter (cosh4 eps=1e-12,
+// 1.65 M records: 25.8 k atomics, 202 us = 0.5 TB/s; profiles/r02t). Each lane takes LEVEL_R records
+// of the chunk (coalesced, LEVEL_R F chains interleaved); the block's wave counts meet in LDS
+// (double-buffered by chunk parity, so two barriers per chunk suffice).
+#ifndef AQ_LEVEL_R
+#define AQ_LEVEL_R 4
+#endif
+constexpr int LEVEL_R = AQ_LEVEL_R;
+
 template <int FID>
 __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
                                                     unsigned* __restrict__ n_out, unsigned cap_out, double eps,
                                                     int depth, int max_depth, LevelPart* __restrict__ parts,
                                                     const ExpPair* __restrict__ gtab) {
+    constexpr int R = LEVEL_R;
     __shared__ ExpEntry tab[128];
     __shared__ double s_h[4], s_l[4];
     __shared__ unsigned s_t[4], s_a[4], s_e[4];
+    __shared__ unsigned s_wc[2][4], s_base[2];
     stage_exp_table(tab, gtab);
     __syncthreads();
     double hi = 0.0, lo = 0.0;
     unsigned tasks = 0, leaves = 0, err = 0;
-    const unsigned stride = gridDim.x * blockDim.x;
-    for (unsigned base = blockIdx.x * blockDim.x; base < n_in; base += stride) {
-        const unsigned i = base + threadIdx.x;
-        const bool active = i < n_in;
-        const Rec rc = active ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
-        const double x[1] = {(rc.l + rc.r) / 2};                         // :187
-        double f[1];
-        integrand_k<FID, 1>(x, f, tab);                                  // :188
-        const double mid = x[0], fmid = f[0];
-        const double lrarea = (rc.fl + rc.fr) * (rc.r - rc.l) / 2;       // :185
-        const double larea = (rc.fl + fmid) * (mid - rc.l) / 2;          // :189
-        const double rarea = (fmid + rc.fr) * (rc.r - mid) / 2;          // :190
-        const bool ref = active && fabs((larea + rarea) - lrarea) > eps; // :191
-        bool refine = false;
-        if (active) {
-            ++tasks;
-            if (!ref) {
-                dd_add(hi, lo, larea + rarea);                           // :199 -> :149
-                ++leaves;
-            } else if (depth + 1 >= max_depth) {
-                err |= ERRB_DEPTH;
-            } else {
-                refine = true;
+    const unsigned w = threadIdx.x >> 6;
+    const unsigned chunk = 256u * R;
+    unsigned parity = 0;
+    // the loop bound depends on blockIdx only: every thread of the block runs every chunk (barriers)
+    for (unsigned base = blockIdx.x * chunk; base < n_in; base += gridDim.x * chunk, parity ^= 1u) {
+        Rec rc[R];
+        bool active[R];
+        double x[R], f[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const unsigned i = base + (unsigned)k * 256u + threadIdx.x;
+            active[k] = i < n_in;
+            rc[k] = active[k] ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
+            x[k] = (rc[k].l + rc[k].r) / 2;                              // :187
+        }
+        integrand_k<FID, R>(x, f, tab);                                  // :188
+        bool refine[R];
+        unsigned long long m[R];
+        unsigned c[R + 1];
+        c[0] = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const double mid = x[k], fmid = f[k];
+            const double lrarea = (rc[k].fl + rc[k].fr) * (rc[k].r - rc[k].l) / 2;   // :185
+            const double larea = (rc[k].fl + fmid) * (mid - rc[k].l) / 2;            // :189
+            const double rarea = (fmid + rc[k].fr) * (rc[k].r - mid) / 2;            // :190
+            const bool ref = active[k] && fabs((larea + rarea) - lrarea) > eps;       // :191
+            refine[k] = false;
+            if (active[k]) {
+                ++tasks;
+                if (!ref) {
+                    dd_add(hi, lo, larea + rarea);                       // :199 -> :149
+                    ++leaves;
+                } else if (depth + 1 >= max_depth) {
+                    err |= ERRB_DEPTH;
+                } else {
+                    refine[k] = true;
+                }
             }
+            m[k] = __ballot(refine[k]);
+            c[k + 1] = c[k] + (unsigned)__popcll(m[k]);
         }
-        const unsigned long long mask = __ballot(refine);
-        const unsigned cnt = (unsigned)__popcll(mask);
-        unsigned wbase = 0;
-        if (cnt) {
-            if (lane_id() == 0) wbase = atomicAdd(n_out, 2u * cnt);
-            wbase = __shfl(wbase, 0, 64);
+        // one atomic for the block's chunk
+        if (lane_id() == 0) s_wc[parity][w] = c[R];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned tot = s_wc[parity][0] + s_wc[parity][1] + s_wc[parity][2] + s_wc[parity][3];
+            s_base[parity] = tot ? atomicAdd(n_out, 2u * tot) : 0u;
         }
-        if (refine) {
-            const unsigned pos = wbase + 2u * mbcnt(mask);
-            if (pos + 1 < cap_out) {
-                out[pos] = Rec{rc.l, mid, rc.fl, fmid};                  // [l, mid]  (:192-194)
-                out[pos + 1] = Rec{mid, rc.r, fmid, rc.fr};              // [mid, r]  (:195-197)
-            } else {
-                err |= ERRB_OVERFLOW;
+        __syncthreads();
+        unsigned off = s_base[parity];
+        for (unsigned v = 0; v < w; ++v) off += 2u * s_wc[parity][v];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (refine[k]) {
+                const unsigned pos = off + 2u * (c[k] + mbcnt(m[k]));
+                if (pos + 1 < cap_out) {
+                    out[pos] = Rec{rc[k].l, x[k], rc[k].fl, f[k]};       // [l, mid]  (:192-194)
+                    out[pos + 1] = Rec{x[k], rc[k].r, f[k], rc[k].fr};   // [mid, r]  (:195-197)
+                } else {
+                    err |= ERRB_OVERFLOW;
+                }
             }
         }
     }
     wave_sum_dd(hi, lo);
     const unsigned wt = wave_sum_u(tasks), wl = wave_sum_u(leaves), we = wave_or_u(err);
-    const unsigned w = threadIdx.x >> 6;
     if (lane_id() == 0) { s_h[w] = hi; s_l[w] = lo; s_t[w] = wt; s_a[w] = wl; s_e[w] = we; }
     __syncthreads();
     if (threadIdx.x == 0) {
