@@ -183,6 +183,14 @@ int aq_integrate_levels(aq_ctx *ctx, const aq_problem *p, aq_result *res, uint64
 int aq_frontier_root(aq_ctx *ctx, int integrand, double a, double b, double *d_out);
 int aq_level_step(aq_ctx *ctx, int integrand, const double *d_in, uint32_t n_in, double *d_out, uint32_t cap_out,
                   double eps, int depth, int max_depth, uint32_t *d_n_out, double *d_acc);
+/* The same step with the input count read on the DEVICE from *d_n_in (a counter a previous step
+ * wrote), so levels chain on the stream with no host round trip (ppls_amd/frontier.py syncs only
+ * every few levels, or at rebalancing levels). n_in_max bounds *d_n_in (it sizes the grid; blocks
+ * past the real count exit at once). *d_n_out is NOT zeroed: the caller zeroes the counters once
+ * (one array of per-level counts: level d reads counts[d] and appends to counts[d + 1]). */
+int aq_level_step_chained(aq_ctx *ctx, int integrand, const double *d_in, const uint32_t *d_n_in, uint32_t n_in_max,
+                          double *d_out, uint32_t cap_out, double eps, int depth, int max_depth, uint32_t *d_n_out,
+                          double *d_acc);
 
 /* Per-level task / accepted histograms of the last aq_integrate* call (levels 0..maxlev-1). */
 int aq_level_histogram(aq_ctx *ctx, uint64_t *tasks_per_level, uint64_t *leaves_per_level, int maxlev);

@@ -17,7 +17,7 @@ EXPORTS = (
     "aq_exact_round", "aq_max_integrals_per_launch", "aq_integrate_many_async", "aq_integrate_mixed_async",
     "aq_synchronize", "aq_gather_results", "aq_gather_exact", "aq_integrate_levels", "aq_level_histogram",
     "aq_tasks_per_cu", "aq_integrate_batch", "aq_eval_integrand", "aq_eval_cosh", "aq_kernel_timing",
-    "aq_kernel_time", "aq_set_diagnostics", "aq_diagnostics", "aq_frontier_root", "aq_level_step",
+    "aq_kernel_time", "aq_set_diagnostics", "aq_diagnostics", "aq_frontier_root", "aq_level_step", "aq_level_step_chained",
     "aq_group_create", "aq_group_unique_id", "aq_group_join", "aq_group_destroy", "aq_group_size",
     "aq_integrate_group", "aq_print_reference", "aq_print_reference_procs",
 )
@@ -100,6 +100,8 @@ def load(build_if_missing=True):
         "aq_print_reference_procs": ([vp, c_dbl, up, c_int], None),
         "aq_frontier_root": ([vp, c_int, c_dbl, c_dbl, vp], c_int),
         "aq_level_step": ([vp, c_int, vp, ctypes.c_uint32, vp, ctypes.c_uint32, c_dbl, c_int, c_int, vp, vp], c_int),
+        "aq_level_step_chained": ([vp, c_int, vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32, c_dbl, c_int, c_int, vp, vp],
+                                  c_int),
         "aq_group_create": ([ctypes.POINTER(vp), c_int, ctypes.POINTER(vp)], c_int),
         "aq_group_unique_id": ([vp], c_int),
         "aq_group_join": ([vp, c_int, c_int, vp, ctypes.POINTER(vp)], c_int),

@@ -208,8 +208,12 @@ template <int FID>
 __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
                                                     unsigned* __restrict__ n_out, unsigned cap_out, double eps,
                                                     int depth, int max_depth, LevelPart* __restrict__ parts,
-                                                    const ExpPair* __restrict__ gtab) {
+                                                    const ExpPair* __restrict__ gtab,
+                                                    const unsigned* __restrict__ n_in_dev) {
     constexpr int R = LEVEL_R;
+    // chained levels: the count a previous step appended (read once; uniform), clamped to n_in = the
+    // host's bound (<= the input buffer's capacity; a count beyond it was flagged as an overflow)
+    if (n_in_dev) n_in = min(*n_in_dev, n_in);
     __shared__ ExpEntry tab[128];
     __shared__ double s_h[4], s_l[4];
     __shared__ unsigned s_t[4], s_a[4], s_e[4];
@@ -299,20 +303,46 @@ __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, 
     }
 }
 
-__global__ __launch_bounds__(64) void k_level_fold(const LevelPart* __restrict__ parts, int nparts,
-                                                   double* __restrict__ acc) {
-    if (threadIdx.x != 0) return;
-    double H = acc[0], L = acc[1], T = acc[2], A = acc[3], lev = acc[5];
-    unsigned E = (unsigned)acc[4];
-    for (int i = 0; i < nparts; ++i) {
-        const LevelPart& p = parts[i];
+// 256 threads each fold an interleaved share of the rows in row order, then a fixed pairwise tree
+// (strides 128 .. 1) folds the 256 partials: the same order for a given row count (deterministic).
+// One thread folding every row had cost 1.1 ms for the 4096 rows of a chained wide level, a serial
+// fold of the 256 partials 18 us per level (profiles/r02u, r02v).
+constexpr int FOLD_T = 256;
+__global__ __launch_bounds__(FOLD_T) void k_level_fold(const LevelPart* __restrict__ parts, int nparts,
+                                                       double* __restrict__ acc) {
+    __shared__ double s_h[FOLD_T], s_l[FOLD_T], s_t[FOLD_T], s_a[FOLD_T], s_v[FOLD_T];
+    __shared__ unsigned s_e[FOLD_T];
+    const int t = threadIdx.x;
+    double H = 0.0, L = 0.0, T = 0.0, A = 0.0, lev = 0.0;
+    unsigned E = 0;
+    for (int i = t; i < nparts; i += FOLD_T) {
+        const LevelPart p = parts[i];
         dd_add_dd(H, L, p.hi, p.lo);
         T += p.tasks;
         A += p.leaves;
         E |= (unsigned)p.err;
         lev = fmax(lev, p.levels);
     }
-    acc[0] = H; acc[1] = L; acc[2] = T; acc[3] = A; acc[4] = (double)E; acc[5] = lev;
+    s_h[t] = H; s_l[t] = L; s_t[t] = T; s_a[t] = A; s_v[t] = lev; s_e[t] = E;
+    __syncthreads();
+    for (int s = FOLD_T / 2; s > 0; s >>= 1) {
+        if (t < s) {
+            double h = s_h[t], l = s_l[t];
+            dd_add_dd(h, l, s_h[t + s], s_l[t + s]);
+            s_h[t] = h; s_l[t] = l;
+            s_t[t] += s_t[t + s];
+            s_a[t] += s_a[t + s];
+            s_v[t] = fmax(s_v[t], s_v[t + s]);
+            s_e[t] |= s_e[t + s];
+        }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    H = acc[0]; L = acc[1];
+    dd_add_dd(H, L, s_h[0], s_l[0]);
+    acc[0] = H; acc[1] = L; acc[2] += s_t[0]; acc[3] += s_a[0];
+    acc[4] = (double)((unsigned)acc[4] | s_e[0]);
+    acc[5] = fmax(acc[5], s_v[0]);
 }
 
 template <int FID>

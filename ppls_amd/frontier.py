@@ -85,6 +85,15 @@ class HipStepper:
                                         float(eps), int(depth), int(max_depth), nout.data_ptr(), acc.data_ptr()),
                "aq_level_step")
 
+    def chain_step(self, integrand, fin, counts, depth, n_max, fout, cap, eps, max_depth, acc):
+        """The level step reading its input count from counts[depth] on the device and appending to
+        counts[depth + 1]: levels chain on the stream with no host round trip."""
+        base = counts.data_ptr()
+        _check(self.ctx.L.aq_level_step_chained(self.ctx._h, integrand, fin.data_ptr(), base + 4 * depth, int(n_max),
+                                                fout.data_ptr(), int(cap), float(eps), int(depth), int(max_depth),
+                                                base + 4 * (depth + 1), acc.data_ptr()),
+               "aq_level_step_chained")
+
     def sync(self):
         self.ctx.synchronize()
 
@@ -103,10 +112,19 @@ class FrontierResult:
     max_frontier: int = 0
 
 
+CHAIN_LEVELS = 4   # one GPU: levels chained on the device between host looks at the frontier size
+
+
 def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebalance_every: int = 1,
               capacity: int = 1 << 22) -> FrontierResult:
     """One integral over every rank of `group` (torch.distributed, initialised by the caller; a
-    single process runs without one). Collective: every rank calls it with the same arguments."""
+    single process runs without one). Collective: every rank calls it with the same arguments.
+
+    A stepper with `chain_step` (HipStepper) keeps the per-level counts on the device and chains the
+    levels between sync points -- every `rebalance_every` levels with several ranks (where the sizes
+    are exchanged and records moved), every CHAIN_LEVELS levels on one -- so the host reads the
+    frontier size once per sync point instead of once per level. Steppers without it (the CPU
+    restatement in the tests) sync every level."""
     problem = problem or Problem()
     if stepper is None:
         raise AquadError("frontier.integrate needs a stepper (HipStepper(ctx) on the GPU)")
@@ -120,29 +138,49 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     dev = stepper.device
     comm_dev = dev if (distributed and dist.get_backend(group) == "nccl") else torch.device("cpu")
 
+    chain = getattr(stepper, "chain_step", None) if dev.type == "cuda" else None
+    sync_every = rebalance_every if world > 1 else CHAIN_LEVELS
     fronts = [torch.empty((capacity, REC), dtype=torch.float64, device=dev) for _ in range(2)]
     nout = torch.zeros(1, dtype=torch.int32, device=dev)
     acc = torch.zeros(8, dtype=torch.float64, device=dev)
+    n = 1 if rank == 0 else 0
+    counts = None
+    if chain is not None:
+        counts = torch.zeros(max_depth + 3, dtype=torch.int32, device=dev)   # counts[d]: records at level d
+        counts[0] = n
     if dev.type == "cuda":
         # the zeroing ran on torch's stream, the level steps run on the engine's own stream: order them
         torch.cuda.synchronize(dev)
     cur = 0
-    n = 0
     if rank == 0:
         stepper.root(integrand, problem.a, problem.b, fronts[cur])
-        n = 1
     depth = 0
     rebalances = moved = 0
     max_front = 1
     per_level = []
+    bound = n   # chained: an upper bound of this rank's current frontier (children <= 2 x parents)
     while True:
         nxt = 1 - cur
         # a local failure is carried through the size exchange as a negative count, so every rank
         # raises together instead of the others waiting in the collective (one all-gather per level)
         err = ""
+        synced = True
         if depth >= max_depth + 1:
             err = "maximum refinement depth reached"
             produced = 0
+        elif chain is not None:
+            try:
+                chain(integrand, fronts[cur], counts, depth, bound, fronts[nxt], capacity, problem.eps, max_depth, acc)
+            except AquadError as e:
+                err = str(e)
+            bound = min(2 * bound, capacity)
+            synced = bool(err) or (depth + 1) % sync_every == 0
+            produced = 0
+            if synced and not err:
+                stepper.sync()
+                produced = int(counts[depth + 1].item())
+                if produced > capacity:
+                    err = f"capacity exceeded: {produced} > {capacity}"
         else:
             try:
                 stepper.step(integrand, fronts[cur], n, fronts[nxt], capacity, problem.eps, depth, max_depth, nout,
@@ -153,15 +191,19 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
                 err, produced = str(e), 0
             if not err and produced > capacity:
                 err = f"capacity exceeded: {produced} > {capacity}"
-        per_level.append(n)
-        cur, n, depth = nxt, (0 if err else produced), depth + 1
-        counts = torch.tensor([-1 if err else n], dtype=torch.int64, device=comm_dev)
+            per_level.append(n)
+        cur, depth = nxt, depth + 1
+        if not synced:
+            continue
+        n = 0 if err else produced
+        bound = n
+        mysize = torch.tensor([-1 if err else n], dtype=torch.int64, device=comm_dev)
         if distributed:
             gathered = [torch.zeros(1, dtype=torch.int64, device=comm_dev) for _ in range(world)]
-            dist.all_gather(gathered, counts, group=group)
+            dist.all_gather(gathered, mysize, group=group)
             sizes = [int(g.item()) for g in gathered]
         else:
-            sizes = [int(counts.item())]
+            sizes = [-1 if err else n]
         failed = [r for r, v in enumerate(sizes) if v < 0]
         if failed:
             raise AquadError(f"frontier: rank {failed[0]} failed" + (f" ({err})" if err else ""))
@@ -200,10 +242,15 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
                         req.wait()
                 for dst_slice, host in staged:
                     dst_slice.copy_(host)
+                n = send_end + (recv_at - n)      # a rank only sends or only receives
+                bound = n
+                if counts is not None:
+                    counts[depth] = n             # the next chained step reads it on the device
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)   # the next level runs on the engine's own stream
-                n = send_end + (recv_at - n)      # a rank only sends or only receives
     stepper.sync()
+    if counts is not None:
+        per_level = [int(v) for v in counts[:depth].cpu()]
     mine = acc.to(comm_dev)
     if distributed:
         accs = [torch.zeros(8, dtype=torch.float64, device=comm_dev) for _ in range(world)]
@@ -214,6 +261,8 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
         per_level = [int(v) for v in lv.cpu()]
     else:
         accs = [mine]
+    while per_level and per_level[-1] == 0:   # chained levels past the last sync point
+        per_level.pop()
     rows = [a.cpu().numpy() for a in accs]
     hi = lo = 0.0
     for r in rows:

@@ -31,46 +31,68 @@ def rows(pattern):
         return list(csv.DictReader(f))
 
 
+def split_runs(disp, grid_key):
+    """Dispatches of k_level_step in time order -> integrate() calls: a call starts at its root level
+    (one 256-thread block) right after a wider launch. Chained calls may end with a few empty levels."""
+    runs, cur, prev = [], [], None
+    for r in disp:
+        g = int(r[grid_key])
+        if cur and g == 256 and prev is not None and prev > 256:
+            runs.append(cur)
+            cur = []
+        cur.append(r)
+        prev = g
+    if cur:
+        runs.append(cur)
+    return runs
+
+
 def main():
     d = sys.argv[1]
     key = sys.argv[2] if len(sys.argv) > 2 else "cosh4_eps1e-12"
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "trees.json")))[key]
     tpl, lpl = g["tasks_per_level"], g["leaves_per_level"]
     nlev = len(tpl)
-    tr = [r for r in rows(os.path.join(d, "kt", "**", "*kernel_trace.csv")) if KERNEL in r["Kernel_Name"]]
+    tr = [r for r in rows(os.path.join(d, "kt", "**", "*kernel_trace.csv"))]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    runs = len(tr) // nlev
-    if runs == 0:
-        sys.exit("no complete run of %d level dispatches (%d found)" % (nlev, len(tr)))
-    tr = tr[len(tr) - runs * nlev:]   # whole integrate() calls; the first is the warmup
+    runs = [r for r in split_runs([r for r in tr if KERNEL in r["Kernel_Name"]], "Grid_Size_X") if len(r) >= nlev]
+    if not runs:
+        sys.exit("no complete run of %d level dispatches" % nlev)
+    timed = runs[1:] or runs   # the first call is the warmup
+    folds = [r for r in tr if "k_level_fold" in r["Kernel_Name"]]
+    fold_us = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in folds)
 
     def pmc(name):
-        out = [float(r["Counter_Value"]) for r in rows(os.path.join(d, name.lower(), "**", "*counter_collection.csv"))
-               if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name]
-        return out[len(out) - runs * nlev:] if len(out) >= runs * nlev else None
+        rs = [r for r in rows(os.path.join(d, name.lower(), "**", "*counter_collection.csv"))
+              if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name]
+        rs.sort(key=lambda r: int(r["Dispatch_Id"]))
+        rr = [x for x in split_runs(rs, "Grid_Size") if len(x) >= nlev]
+        return [[float(x["Counter_Value"]) for x in run[:nlev]] for run in rr] or None
 
     fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
     levels = []
     for lev in range(nlev):
-        durs = [(int(tr[k * nlev + lev]["End_Timestamp"]) - int(tr[k * nlev + lev]["Start_Timestamp"])) * 1e-9
-                for k in range(1, runs)] or [(int(tr[lev]["End_Timestamp"]) - int(tr[lev]["Start_Timestamp"])) * 1e-9]
-        t = sorted(durs)[len(durs) // 2]
+        durs = sorted((int(run[lev]["End_Timestamp"]) - int(run[lev]["Start_Timestamp"])) * 1e-9 for run in timed)
+        t = durs[len(durs) // 2]
         n_in, n_out = tpl[lev], 2 * (tpl[lev] - lpl[lev])
         alg = REC * (n_in + n_out)
         e = {"level": lev, "records_in": n_in, "records_out": n_out, "us": round(t * 1e6, 2),
              "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1), "hbm_frac_alg": round(alg / t / HBM_PEAK, 4),
              "fp64_frac": round(FLOP * n_in / t / FP64_PEAK, 4)}
         if fetch and write:
-            hb = [(2 * fetch[k * nlev + lev] + write[k * nlev + lev]) * 1024 for k in range(runs)]
-            e["hbm_bytes_measured"] = sorted(hb)[len(hb) // 2]
+            hb = sorted((2 * f[lev] + w[lev]) * 1024 for f, w in zip(fetch, write))
+            e["hbm_bytes_measured"] = hb[len(hb) // 2]
         levels.append(e)
     tot_t = sum(e["us"] for e in levels) * 1e-6
     tot_b = sum(e["alg_bytes"] for e in levels)
     widest = max(levels, key=lambda e: e["records_in"])
-    print(json.dumps({"kernel": KERNEL, "workload": key, "levels": nlev, "runs_timed": max(runs - 1, 1),
+    print(json.dumps({"kernel": KERNEL, "workload": key, "levels": nlev, "runs_timed": len(timed),
+                      "dispatches_per_run": [len(r) for r in runs],
                       "sum_level_us": round(tot_t * 1e6, 1), "alg_bytes_total": tot_b,
                       "alg_GBps_overall": round(tot_b / tot_t / 1e9, 1),
                       "fp64_frac_overall": round(FLOP * sum(tpl) / tot_t / FP64_PEAK, 4),
+                      "fold_us_median": fold_us[len(fold_us) // 2] if fold_us else None,
+                      "fold_us_max": fold_us[-1] if fold_us else None,
                       "widest_level": widest, "per_level": levels}, indent=1))
 
 
