@@ -80,6 +80,10 @@ constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its vie
 #define AQ_GIVE_ROUNDS 32   // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
+#ifndef AQ_SKEWED_GIVE
+#define AQ_SKEWED_GIVE 4
+#endif
+constexpr int SKEWED_GIVE = AQ_SKEWED_GIVE;   // give rounds for the skewed built-in integrand (sin(1/x))
 // (lone-integral launches, whose waves run only ~3-13 rounds of one share, measured with give /
 // poll intervals of 2-16 rounds and GIVE_MIN 32-64: all slower, 1e-10 up to 2x -- HBM donations
 // and bursts cut short cost more than the balance they buy; profiles/r02_ab)
@@ -549,7 +553,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
     bool counted_idle = false;
     bool fresh = true;            // before this wave's first seeding
-    constexpr unsigned give_rounds = GIVE_ROUNDS, poll_rounds = POLL_ROUNDS, give_min = GIVE_MIN;
+    // sin(1/x) (config 4) piles nearly all of its tree into one small region: its waves look for idle
+    // siblings every SKEWED_GIVE rounds (a lone integral 79 -> 70 us at 4; cosh4 keeps 32, where 4 cost
+    // the eps=1e-12 lone tree 47 -> 61 us and the bench 0.6 %; profiles/r02_ab/fast_give_poll*.txt)
+    constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE : (unsigned)GIVE_ROUNDS;
+    constexpr unsigned poll_rounds = POLL_ROUNDS, give_min = GIVE_MIN;
     unsigned poll_ctr = wid * (poll_rounds / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
