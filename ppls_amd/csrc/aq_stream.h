@@ -84,6 +84,14 @@ constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle sibli
 #define AQ_SKEWED_GIVE 4
 #endif
 constexpr int SKEWED_GIVE = AQ_SKEWED_GIVE;   // give rounds for the skewed built-in integrand (sin(1/x))
+#ifndef AQ_SKEWED_POLL
+#define AQ_SKEWED_POLL AQ_POLL_ROUNDS
+#endif
+constexpr int SKEWED_POLL = AQ_SKEWED_POLL;
+#ifndef AQ_SKEWED_GIVE_MIN
+#define AQ_SKEWED_GIVE_MIN AQ_GIVE_MIN
+#endif
+constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 // (lone-integral launches, whose waves run only ~3-13 rounds of one share, measured with give /
 // poll intervals of 2-16 rounds and GIVE_MIN 32-64: all slower, 1e-10 up to 2x -- HBM donations
 // and bursts cut short cost more than the balance they buy; profiles/r02_ab)
@@ -557,7 +565,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // siblings every SKEWED_GIVE rounds (a lone integral 79 -> 70 us at 4; cosh4 keeps 32, where 4 cost
     // the eps=1e-12 lone tree 47 -> 61 us and the bench 0.6 %; profiles/r02_ab/fast_give_poll*.txt)
     constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE : (unsigned)GIVE_ROUNDS;
-    constexpr unsigned poll_rounds = POLL_ROUNDS, give_min = GIVE_MIN;
+    constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL : (unsigned)POLL_ROUNDS;
+    constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN : (unsigned)GIVE_MIN;
     unsigned poll_ctr = wid * (poll_rounds / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
