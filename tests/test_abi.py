@@ -51,6 +51,8 @@ def test_strerror_and_arg_validation(lib):
     # NULL context / arguments are rejected before any device call
     assert lib.aq_integrate(None, None, None) == -1
     assert lib.aq_fetch(None, 0, None) == -1
+    assert lib.aq_level_step(None, 0, None, 0, None, 0, 1e-3, 0, 64, None, None) == -1
+    assert lib.aq_level_step_chained(None, 0, None, None, 0, None, 0, 1e-3, 0, 64, None, None) == -1
     n = ctypes.c_int(-1)
     rc = lib.aq_device_count(ctypes.byref(n))
     assert (rc == 0) == (n.value > 0)
