@@ -27,14 +27,14 @@ def main():
     args = ap.parse_args()
     trees = json.load(open(os.path.join(ROOT, "tests", "golden", "trees.json")))
     batch = json.load(open(os.path.join(ROOT, "tests", "golden", "batch.json")))
-    from oracle import pyoracle as O
+    from tools.bench_batch import splitmix64_bounds   # the C3 generator (no oracle in tools/)
     ctx = Context(0)
     ctx.set_level_histograms(False)
     out = {"lib": os.environ.get("AQ_LIB", "default")}
     g3 = trees["cosh4_eps1e-3"]
     ctx.integrate_many_async(np.zeros(32), np.full(32, 5.0), 1e-3)
     out["eps1e-3_x32_ok"] = all((r.tasks, r.accepted) == (g3["tasks"], g3["leaves"]) for r in (ctx.fetch(i) for i in range(32)))
-    a, b = O.batch_bounds(max(256, args.c3))
+    a, b = splitmix64_bounds(max(256, args.c3))
     ctx.integrate_many_async(a[:256], b[:256], 1e-3)
     out["batch256_ok"] = [ctx.fetch(i).accepted for i in range(256)] == batch["leaves_eps1e-3_first256"]
     tag = {1e-10: "cosh4_eps1e-10", 1e-12: "cosh4_eps1e-12", 1e-8: "cosh4_eps1e-8"}[args.eps]
