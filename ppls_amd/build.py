@@ -20,7 +20,13 @@ CLI = os.path.join(OUT, "aquad")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ARCH = os.environ.get("PPLS_AMD_ARCH", "gfx950")
 
+# -amdgpu-atomic-optimizer-strategy=None: every device atomic here is already issued by one lane (the
+# kernels aggregate by hand); LLVM's optimizer wraps each in a ballot / mbcnt / readfirstlane sequence
+# whose broadcast of the returned value waits for the atomic at once -- it had made k_stream's job
+# claim (meant to stay in flight across a job) a full round trip. r02 A/B: bench -1.5 %, lone
+# integral 26.5 -> 25.7 us (profiles/r02_ab/sload_atomic_opt.txt).
 HIP_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-I", CSRC]
 
 SOURCES = [os.path.join(CSRC, "aquad.hip")]

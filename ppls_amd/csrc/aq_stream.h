@@ -408,6 +408,22 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
     __builtin_amdgcn_wave_barrier();   // reconverge: keeps the caller's wave state out of this join
 }
 
+// {a, b} of integral p through the scalar data cache (a READ: s_load; the host wrote the bounds before
+// the launch and the scalar cache starts every kernel invalidated). p is wave-uniform.
+#ifndef AQ_SLOAD_BOUNDS
+#define AQ_SLOAD_BOUNDS 1
+#endif
+constexpr bool SLOAD_BOUNDS = AQ_SLOAD_BOUNDS != 0;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double2 sload_bounds(const double2* base, int p) {
+    const unsigned long long a64 = (unsigned long long)(base + p);
+    const unsigned long long addr = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(a64 >> 32)) << 32) |
+                                    (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a64);
+    u32x4 r;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(addr) : "memory");
+    return make_double2(__hiloint2double((int)r.y, (int)r.x), __hiloint2double((int)r.w, (int)r.z));
+}
+
 // One slot's six fields from / to ONE LDS address (the slot's a, in bytes): three ds_read2st64_b64
 // / ds_write2st64_b64 at 0 / 50 / 100 / 150 / 200 / 250 x 512 B (LREC = 3200 slots of 8 B per
 // field). The pop waits for its own reads (lgkmcnt(0)) inside the asm -- the compiler cannot count
@@ -555,7 +571,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const bool static_jobs = PCU || P.static_jobs != 0;
     unsigned job = static_jobs ? wid * gridDim.x + bid : w_all;
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
-    unsigned claim = 0;           // lane 0: the prefetched claim
+    unsigned claim = 0;           // lane 0: the prefetched claim (job = W + claim)
     unsigned err = 0;
     bool mixed = false;           // a round met pairs of another integral (never expected)
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
@@ -641,7 +657,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
             }
             if (job_pending) {
-                job = uni(__shfl(claim, 0, 64));
+                job = W + uni(__shfl(claim, 0, 64));   // claims count from W (the first W jobs are dealt)
                 job_pending = false;
             }
             unsigned k = 0;
@@ -752,14 +768,19 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
                 // the bounds load goes out before the claim: waiting for it then leaves the claim (one
                 // contended atomic, not needed before the next job) in flight
-                const double2 ab = PCU ? P.kbounds[p] : P.bounds[p];   // once per job (HBM / L2)
+                // once per job. A scalar load (lgkmcnt), so the wait for it does not also wait for the
+                // previous integral's flush atomics and this job's claim (vmcnt, in issue order), which
+                // stay in flight while the job seeds (C3 eps=1e-3 A/B: profiles/r02_ab/sload_bounds.txt)
+                const double2 ab = PCU ? P.kbounds[p] : (SLOAD_BOUNDS ? sload_bounds(P.bounds, p) : P.bounds[p]);
                 if (static_jobs) {
                     // launches of few integrals cut every integral into one share per wave: wave w seeds share w of
                     // each integral in turn (static stride, no claim). 3072 waves claiming through one
                     // counter cost a 2-integral launch 87 us instead of ~25.
                     job += W;
                 } else if (total_jobs > W) {
-                    if (lane == 0) claim = W + g_add(&qc->jobs.v, 1u);   // next job: latency hides behind this one
+                    // next job: the latency hides behind this one. The raw counter value is kept (W is added
+                    // at the read): any arithmetic on the result here would wait for the atomic at once
+                    if (lane == 0) claim = g_add(&qc->jobs.v, 1u);
                     job_pending = true;
                 } else {
                     // every job was handed out at launch (job = w_all): no claim, so a lone integral's

@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
     ap.add_argument("--k", type=int, default=1, help="integrals per launch")
+    ap.add_argument("--c3", action="store_true", help="splitmix64 bounds (SURVEY C3) instead of [0, 5]")
     args = ap.parse_args()
     ctx = Context(0)
     ctx.set_level_histograms(False)
@@ -68,7 +69,12 @@ def main():
         if args.k == 1:
             r = ctx.integrate(Problem(eps=args.eps))
         else:
-            ctx.integrate_many_async(np.zeros(args.k), np.full(args.k, 5.0), args.eps)
+            if args.c3:
+                from tools.bench_batch import splitmix64_bounds
+                a, b = splitmix64_bounds(args.k)
+                ctx.integrate_many_async(a, b, args.eps)
+            else:
+                ctx.integrate_many_async(np.zeros(args.k), np.full(args.k, 5.0), args.eps)
             r = ctx.fetch(args.k - 1)
         d, f = ctx.diagnostics()
         res.append(summarize(d, f))

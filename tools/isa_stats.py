@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def compile_asm(defs, out):
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-c",
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-c", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "--cuda-device-only", "-S", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "ppls_amd", "csrc"),
            '-DAQ_USER_F_HEADER="%s"' % os.path.join(ROOT, "ppls_amd", "csrc", "plugins", "aq_user_gauss.h"),
            "-Rpass-analysis=kernel-resource-usage", "-o", out] + defs + [os.path.join(ROOT, "ppls_amd", "csrc", "aquad.hip")]
