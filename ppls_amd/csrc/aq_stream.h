@@ -67,6 +67,18 @@ struct DtField {
 #define AQ_S_W 2
 #endif
 constexpr int S_W = AQ_S_W;              // seed depth D = floor(log2 V) + S_W: 3 or 4 positions per share
+#ifndef AQ_JOB_RUN_MAX
+#define AQ_JOB_RUN_MAX 16
+#endif
+constexpr int JOB_RUN_MAX = AQ_JOB_RUN_MAX;   // most jobs one claim takes (whole-integral jobs only)
+#ifndef AQ_S_W1
+#define AQ_S_W1 2
+#endif
+// seed depth of a job: floor(log2 V) + S_W for V = shares x shards virtual workers; a whole-integral
+// job (V = 1, tiny trees of big batches) seeds at S_W1 (its partition is the whole tree at any depth)
+__host__ __device__ constexpr int seed_depth(unsigned long long V) {
+    return V <= 1ull ? AQ_S_W1 : 63 - __builtin_clzll(V) + S_W;
+}
 #ifndef AQ_GIVE_MIN
 #define AQ_GIVE_MIN 96
 #endif
@@ -529,7 +541,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
             shares_main = h;
-            D_main = 63 - __builtin_clzll((unsigned long long)h * (unsigned long long)P.nshards) + S_W;
+            D_main = seed_depth((unsigned long long)h * (unsigned long long)P.nshards);
         }
     }
     const unsigned W = gridDim.x * (unsigned)NW;
@@ -544,7 +556,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // (only where an integral is already several jobs: whole-integral jobs of tiny trees are short)
     const unsigned tail_from = shares_main >= 8u ? (unsigned)P.tail_from : (unsigned)P.nprob;
     const unsigned shares_tail = min(shares_main * (unsigned)P.tail_mult, W);
-    const int D_tail = 63 - __builtin_clzll((unsigned long long)shares_tail * (unsigned long long)P.nshards) + S_W;
+    const int D_tail = seed_depth((unsigned long long)shares_tail * (unsigned long long)P.nshards);
     const unsigned main_jobs = tail_from * shares_main;
     const unsigned total_jobs = main_jobs + ((unsigned)P.nprob - tail_from) * shares_tail;
     const unsigned base = wid * WCAP;                            // this wave's ring
@@ -571,7 +583,15 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const bool static_jobs = PCU || P.static_jobs != 0;
     unsigned job = static_jobs ? wid * gridDim.x + bid : w_all;
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
-    unsigned claim = 0;           // lane 0: the prefetched claim (job = W + claim)
+    unsigned claim = 0;           // lane 0: the prefetched claim (jobs W + claim .. + jpc - 1)
+    // jobs per claim. Whole-integral jobs of a big batch are short (C3 at eps=1e-3: ~1 400 tasks), and
+    // one claim each made the job counter a serial fan-in (65536 claims on one line, ~10 ns each: a
+    // static deal of the same launch ran 815 -> 543 us). Such launches claim a run of consecutive
+    // jobs at once -- at least 4 claims per wave stay, for the balance -- one job otherwise.
+    const unsigned jpc = (!static_jobs && shares_main == 1u && P.nshards == 1 && JOB_RUN_MAX > 1)
+                             ? max(1u, min((unsigned)JOB_RUN_MAX, total_jobs / (4u * W)))
+                             : 1u;
+    unsigned job_end = job + 1u;  // end of the claimed run `job` belongs to
     unsigned err = 0;
     bool mixed = false;           // a round met pairs of another integral (never expected)
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
@@ -658,6 +678,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             if (job_pending) {
                 job = W + uni(__shfl(claim, 0, 64));   // claims count from W (the first W jobs are dealt)
+                job_end = job + jpc;
                 job_pending = false;
             }
             unsigned k = 0;
@@ -778,10 +799,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     // counter cost a 2-integral launch 87 us instead of ~25.
                     job += W;
                 } else if (total_jobs > W) {
-                    // next job: the latency hides behind this one. The raw counter value is kept (W is added
-                    // at the read): any arithmetic on the result here would wait for the atomic at once
-                    if (lane == 0) claim = g_add(&qc->jobs.v, 1u);
-                    job_pending = true;
+                    if (job + 1u < job_end) {
+                        ++job;   // the next job of this wave's claimed run: no atomic
+                    } else {
+                        // next run: the latency hides behind this job. The raw counter value is kept (W is
+                        // added at the read): any arithmetic on the result here would wait for the atomic
+                        if (lane == 0) claim = g_add(&qc->jobs.v, jpc);
+                        job_pending = true;
+                    }
                 } else {
                     // every job was handed out at launch (job = w_all): no claim, so a lone integral's
                     // 3072 waves do not queue on one atomic before their first F evaluation
