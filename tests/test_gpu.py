@@ -204,6 +204,26 @@ def test_batch_front_end(ctx, batch_golden, oracle):
     assert np.all(np.abs(area - want) <= AREA_RTOL * np.abs(want))
 
 
+def test_batch_front_end_multi_chunk(ctx, batch_golden, oracle):
+    """A batch of three launches' worth (2 x 65536 + 1000 integrals): the rows of every chunk are
+    unpacked while the next one runs; the first 256 against the golden fixture, the last chunk's
+    against the oracle. A bad bound in the second chunk fails the call and leaves the context usable."""
+    from ppls_amd import AquadError
+    n = 2 * 65536 + 1000
+    a, b = oracle.batch_bounds(n)
+    area, tasks, acc = ctx.integrate_batch(a, b, 1e-3)
+    assert [int(v) for v in acc[:256]] == batch_golden["leaves_eps1e-3_first256"]
+    assert (tasks == 2 * acc - 1).all()
+    oa, ot, ol = oracle.integrate_batch(a[-200:], b[-200:], 1e-3)
+    assert list(acc[-200:]) == list(ol) and list(tasks[-200:]) == list(ot)
+    bad_a = a.copy()
+    bad_a[70000] = np.nan
+    with pytest.raises(AquadError):
+        ctx.integrate_batch(bad_a, b, 1e-3)
+    area2, _, acc2 = ctx.integrate_batch(a[:64], b[:64], 1e-3)
+    assert list(acc2) == list(acc[:64])
+
+
 def test_cli_reference_output(trees):
     from ppls_amd import build
     build.build()
