@@ -63,7 +63,9 @@ typedef struct {
 
 /* Replaces farmer()'s return value and the global tasks_per_process[] (:72, :101, :162). */
 typedef struct {
-    double area;        /* Σ accepted larea+rarea (:199 sent, :149 summed): correctly rounded exact sum */
+    double area;        /* Σ accepted larea+rarea (:199 sent, :149 summed): the exact sum of the workers'
+                           partials (per-lane double sums in the persistent kernel), rounded once -- within
+                           a few ulp of the exact leaf sum, last bits schedule-dependent */
     uint64_t tasks;     /* intervals evaluated = Σ tasks_per_process (:162) */
     uint64_t accepted;  /* accepted subintervals (tag-1 area messages, :201) */
     uint32_t levels;    /* 1 + deepest refinement level reached */
@@ -117,6 +119,10 @@ int aq_integrate(aq_ctx *ctx, const aq_problem *p, aq_result *res);
  * area/tasks/accepted over all shards (the caller's all-reduce, or aq_integrate_group) gives
  * exactly the single-GPU result. */
 int aq_integrate_shard(aq_ctx *ctx, const aq_problem *p, int shard, int nshards, aq_result *res);
+/* The same shard, returned as its exact row (int64[AQ_EXACT_ROW], the layout of aq_fetch_exact): the
+ * input of a caller's int64 all-reduce (ppls_amd/dist.py). Blocking, internal slot like
+ * aq_integrate_shard; the return code carries the row's error bits (the row is written either way). */
+int aq_integrate_shard_exact(aq_ctx *ctx, const aq_problem *p, int shard, int nshards, int64_t *row);
 
 /* ---- multi-GPU over RCCL (replaces the MPI layer, :145-171, and `result += buff[0]`, :149) ----
  * A group is a set of contexts, one per GPU, joined by RCCL communicators over xGMI. Either one
@@ -200,7 +206,12 @@ int aq_level_histogram(aq_ctx *ctx, uint64_t *tasks_per_level, uint64_t *leaves_
 int aq_tasks_per_cu(aq_ctx *ctx, uint64_t *out, int cap);
 
 /* Batch front end (SURVEY config 3): n independent integrals [a[i], b[i]] of one integrand.
- * Per-integral area / accepted / tasks (any may be NULL). */
+ * Per-integral area / accepted / tasks (any may be NULL). NOTE the output order: accepted BEFORE
+ * tasks (round 1's header had a single `accepted` output; both are uint64_t*, so a caller written
+ * against another order compiles and gets the arrays swapped). The integrals run in launches of up
+ * to aq_max_integrals_per_launch(); each launch's bounds are validated just before it is enqueued,
+ * so a bad bound in a later launch returns AQ_EINVAL after the earlier launches ran: the outputs
+ * are then unspecified (not all-or-nothing). */
 int aq_integrate_batch(aq_ctx *ctx, size_t n, const double *a, const double *b, double eps, int integrand,
                        double *area, uint64_t *accepted, uint64_t *tasks);
 

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("AQ_LIB") or os.path.join(HERE, "_build", "libaquad.so
 EXPORTS = (
     "aq_device_count", "aq_ctx_create", "aq_ctx_destroy", "aq_strerror", "aq_ctx_num_cus", "aq_ctx_num_workers",
     "aq_ctx_device_bytes", "aq_set_level_histograms", "aq_set_stall_timeout", "aq_user_integrand_name",
-    "aq_integrate", "aq_integrate_shard", "aq_async_slots", "aq_integrate_async", "aq_fetch", "aq_fetch_exact",
+    "aq_integrate", "aq_integrate_shard", "aq_integrate_shard_exact", "aq_async_slots", "aq_integrate_async", "aq_fetch", "aq_fetch_exact",
     "aq_exact_round", "aq_max_integrals_per_launch", "aq_integrate_many_async", "aq_integrate_mixed_async",
     "aq_synchronize", "aq_gather_results", "aq_gather_exact", "aq_integrate_levels", "aq_level_histogram",
     "aq_tasks_per_cu", "aq_integrate_batch", "aq_eval_integrand", "aq_eval_cosh", "aq_kernel_timing",
@@ -75,6 +75,7 @@ def load(build_if_missing=True):
         "aq_user_integrand_name": ([], ctypes.c_char_p),
         "aq_integrate": ([vp, P, R], c_int),
         "aq_integrate_shard": ([vp, P, c_int, c_int, R], c_int),
+        "aq_integrate_shard_exact": ([vp, P, c_int, c_int, lp], c_int),
         "aq_async_slots": ([], c_int),
         "aq_integrate_async": ([vp, P, c_int, c_int, c_int], c_int),
         "aq_fetch": ([vp, c_int, R], c_int),

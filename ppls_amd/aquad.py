@@ -167,6 +167,15 @@ class Context:
                "aq_integrate_shard")
         return self._result(r)
 
+    def integrate_shard_exact(self, problem: Problem, shard: int, nshards: int) -> np.ndarray:
+        """This shard's exact row (int64[AQ_EXACT_ROW], as fetch_exact), run in the internal slot: no
+        async slot of the caller is touched."""
+        row = np.zeros(_lib.AQ_EXACT_ROW, np.int64)
+        _check(self.L.aq_integrate_shard_exact(self._h, ctypes.byref(problem.c()), int(shard), int(nshards),
+                                               row.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))),
+               "aq_integrate_shard_exact")
+        return row
+
     def integrate_levels(self, problem: Problem) -> Result:
         r = _lib.aq_result()
         t = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)

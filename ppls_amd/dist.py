@@ -62,6 +62,17 @@ def _agree_on_errors(code: int, dev, group) -> None:
         raise AquadError(f"rank {r} failed ({_lib.load().aq_strerror(c).decode() if c < 0 else 'error'}, code {c})", c)
 
 
+def _err_code_from_bits(bits: int) -> int:
+    """The C ABI's error code for a row's device error bits (aq_abi.inc err_from_bits)."""
+    if bits & 1:
+        return -3    # AQ_ETIMEOUT
+    if bits & 2:
+        return -4    # AQ_EOVERFLOW
+    if bits & 4:
+        return -5    # AQ_EDEPTH
+    return -1
+
+
 def combine_rows(row: np.ndarray, group=None, dev=None, err: int = 0) -> Result:
     """All-reduce one rank's exact row into the whole-run result (identical on every rank)."""
     dev = dev or torch.device("cpu")
@@ -104,8 +115,7 @@ def integrate_distributed(problem: Problem, group=None, ctx: Optional[Context] =
     row, err = np.zeros(ROW, np.int64), 0
     try:
         if shard_fn is None:
-            ctx.integrate_async(problem, 0, rank, world)
-            row = ctx.fetch_exact(0)
+            row = ctx.integrate_shard_exact(problem, rank, world)   # internal slot: async slots untouched
         else:
             row = np.asarray(shard_fn(problem, rank, world), np.int64)
     except AquadError as e:
@@ -157,12 +167,17 @@ class HipBatchRunner:
     def run(self, a, b, shards, nshards, eps, integrand) -> np.ndarray:
         if len(a) == 0:
             return np.zeros((0, ROW), np.int64)
+        n = len(a)
+        out = torch.empty((n, ROW), dtype=torch.int64, device=torch.device("cuda", self.ctx.device))
         self.ctx.kernel_timing(True)
-        self.ctx.integrate_mixed_async(a, b, shards, nshards, eps, first_slot=0, integrand=integrand)
-        rows = np.stack([self.ctx.fetch_exact(i) for i in range(len(a))])
-        self.ms, _ = self.ctx.kernel_time()
-        self.ctx.kernel_timing(False)
-        return rows
+        try:
+            self.ctx.integrate_mixed_async(a, b, shards, nshards, eps, first_slot=0, integrand=integrand)
+            # every unit's row in one device gather, one copy back and one synchronisation
+            self.ctx.gather_exact(0, n, out.data_ptr())
+            self.ms, _ = self.ctx.kernel_time()   # synchronises the context's stream
+        finally:
+            self.ctx.kernel_timing(False)
+        return out.cpu().numpy()
 
 
 def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None, shards_per_integral=None,
@@ -220,9 +235,12 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
             my_ms += getattr(runner, "ms", 0.0)
         except AquadError as e:
             err = e.code if e.code else -1
+        # device error bits in the rows (a runner that returns them instead of raising) join the
+        # agreement too: every rank raises together, none is left waiting in the all-reduce below
+        bits = int(np.bitwise_or.reduce(rows[:, XL + 3] >> 32)) if rows.size else 0
+        if bits and not err:
+            err = _err_code_from_bits(bits)
         _agree_on_errors(err, dev, group)
-        if rows.size and int((rows[:, XL + 3] >> 32).max()):
-            raise AquadError("a unit reported device error bits")
         # every rank learns every unit's row: its share of the exact sums and the measured costs
         full = np.zeros((len(units), ROW), np.int64)
         for j, u in enumerate(plan[rank]):

@@ -168,3 +168,38 @@ def test_gloo_batch_whole_integral_units(oracle, rebalance):
     assert all(abs(v - want.area) <= 1e-12 * abs(want.area) for v in area)
     assert per_rank == [6 * want.tasks, 6 * want.tasks]
     assert results[1] == results[0]
+
+
+class _BitsRunner(_OracleBatchRunner):
+    """A runner that returns device error bits in its rows instead of raising (rank 1 only)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def run(self, a, b, shards, nshards, eps, integrand):
+        rows = super().run(a, b, shards, nshards, eps, integrand)
+        if self.rank == 1 and rows.size:
+            rows[0, 71] |= 4 << 32   # ERRB_DEPTH in the levels | error << 32 word
+        return rows
+
+
+def _bits_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        from ppls_amd.aquad import AquadError
+        from ppls_amd.dist import integrate_batch_distributed
+        try:
+            integrate_batch_distributed(np.full(4, 1e-4), np.ones(4), 1e-5, integrand=1, runner=_BitsRunner(rank),
+                                        shards_per_integral=2, window=4, rebalance=False)
+            q.put((rank, "no error"))
+        except AquadError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_batch_error_bits_raise_everywhere():
+    """error bits a runner RETURNS (not raises) on one rank make every rank raise -- the
+    healthy ranks must not be left in the all-reduce."""
+    results = _run(_bits_worker, 2, timeout=120)
+    assert all("rank 1 failed" in results[r] and "depth" in results[r] for r in range(2)), results

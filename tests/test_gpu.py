@@ -592,6 +592,28 @@ def test_rccl_group_single_process(ctx, trees):
             assert _area_ok(r.area, g["area_quad"])
 
 
+def test_group_call_leaves_async_slots_alone(ctx, trees):
+    """aq_integrate_group runs its shard in the internal slot, like aq_integrate: a
+    pending async slot-0 result survives a Group.integrate, and so does one around integrate_shard_exact."""
+    from ppls_amd import Group, Problem
+    g3, g10 = trees["cosh4_eps1e-3"], trees["cosh4_eps1e-10"]
+    with Group([ctx]) as grp:
+        ctx.integrate_async(Problem(eps=1e-3), 0)
+        r = grp.integrate(Problem(eps=1e-10))
+        assert (r.tasks, r.accepted) == (g10["tasks"], g10["leaves"])
+        r0 = ctx.fetch(0)
+        assert (r0.tasks, r0.accepted) == (g3["tasks"], g3["leaves"])
+        r = grp.integrate(Problem(eps=1e-3))   # the internal slot starts from zero again
+        assert (r.tasks, r.accepted) == (g3["tasks"], g3["leaves"])
+    ctx.integrate_async(Problem(eps=1e-3), 0)
+    row = ctx.integrate_shard_exact(Problem(eps=1e-10), 0, 1)
+    assert (int(row[68]), int(row[69])) == (g10["tasks"], g10["leaves"])
+    r0 = ctx.fetch(0)
+    assert (r0.tasks, r0.accepted) == (g3["tasks"], g3["leaves"])
+    r = ctx.integrate(Problem(eps=1e-3))
+    assert (r.tasks, r.accepted) == (g3["tasks"], g3["leaves"])
+
+
 def test_rccl_group_join(ctx, trees):
     """The one-process-per-GPU form (aq_group_unique_id + aq_group_join), as an MPI rank would use it."""
     from ppls_amd import Group, Problem
