@@ -100,6 +100,77 @@ def load_traffic(tasks_per_launch):
         return None
 
 
+def ranks_seen(dist, coll, distributed):
+    """How many ranks the process group really spans: an all-reduce of ones over it (RCCL under nccl),
+    done before timing -- the line's n_gpus is checked against it, not just read from WORLD_SIZE."""
+    if not distributed:
+        return 1
+    import torch
+    one = torch.ones(1, dtype=torch.int64, device=coll)
+    dist.all_reduce(one)
+    return int(one.item())
+
+
+def rank_stats(dist, coll, distributed, kern_ms, launches, tasks, elapsed):
+    """Every rank's kernel time, launches and tasks over the timed region (one all-gather), and the
+    imbalance max / mean of the kernel time and of the tasks (the farmer's per-worker counts, :162)."""
+    import torch
+    mine = torch.tensor([kern_ms, float(launches), float(tasks), elapsed], dtype=torch.float64, device=coll)
+    if distributed:
+        rows = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(rows, mine)
+    else:
+        rows = [mine]
+    rows = [r.cpu().tolist() for r in rows]
+    ms = [r[0] for r in rows]
+    tk = [int(r[2]) for r in rows]
+    mean = lambda v: sum(v) / len(v) if v else 0.0
+    return {"kernel_ms": ms, "launches": [int(r[1]) for r in rows], "tasks": tk, "elapsed_s": [r[3] for r in rows],
+            "kernel_imbalance": max(ms) / mean(ms) if mean(ms) > 0 else None,
+            "task_imbalance": max(tk) / mean(tk) if mean(tk) > 0 else None}
+
+
+def bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, per_launch, ctx_cus, single_ms,
+               single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu):
+    """The one JSON line rank 0 prints (the driver's contract plus roofline, cpu_baseline and the
+    multi-rank fields: backend, ranks_seen -- counted by a collective -- and per-rank kernel time and
+    tasks with their imbalance)."""
+    return {
+        "metric": "accepted subintervals/sec + FP64 F-evals/sec at 1/2/4/8 MI355X, EPSILON=1e-10",
+        "value": accepted_total / elapsed,
+        "unit": "accepted subintervals/s",
+        "f_evals_per_sec": f_evals / elapsed,
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / K,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (analytic integrand, no dataset)",
+        "config": {"workload": "cosh4 on [0,5], EPSILON=%g (BASELINE %s); one step = a batch of %d "
+                               "such integrals, each sharded over the GPUs"
+                               % (args.eps, {1e-10: "configs[1]", 1e-12: "configs[4]"}.get(args.eps, "off-config"), B),
+                   "integrand": "cosh(x)^4 (aquadPartA.c:46)", "a": 0.0, "b": 5.0, "eps": args.eps,
+                   "tasks_per_integral": int(tot[0, 1]), "accepted_per_integral": int(tot[0, 2]),
+                   "parallelism": f"shard{world}" if world > 1 else "single-gpu",
+                   "integrals_per_step": B,
+                   "integrals_per_launch": per_launch,
+                   "workgroups_per_gpu": ctx_cus},
+        "single_integral_kernel_us": single_ms * 1e3 / single_n if single_n else None,
+        "verified": ok,
+        "backend": backend,
+        "ranks_seen": seen,
+        "per_rank": stats,
+        "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(tasks_per_launch),
+                     "kernel": "aq::k_stream<0,false,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
+                     "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": tasks_per_launch},
+        "cpu_baseline": cpu,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -151,6 +222,11 @@ def main():
             dist.all_reduce(h, op=op)
             if h is not t:
                 t.copy_(h)
+
+    backend = dist.get_backend() if distributed else None
+    seen = ranks_seen(dist, coll, distributed)
+    if seen != world:
+        print(f"bench: the process group spans {seen} ranks, WORLD_SIZE={world}", file=sys.stderr)
 
     ctx = Context(dev)
     ctx.set_level_histograms(False)
@@ -216,6 +292,7 @@ def main():
         ctx.gather_results(0, m * B, totals.data_ptr() + done * B * 4 * totals.element_size())
         done += m
     ctx.synchronize()
+    my_tasks = totals[:, 1].sum()           # this rank's tasks (its shards), before the combine
     all_reduce(totals, dist.ReduceOp.SUM)   # shard partials -> whole integrals
     torch.cuda.synchronize()
     barrier()
@@ -224,6 +301,8 @@ def main():
     ctx.kernel_timing(False)
 
     elapsed = t1 - t0
+    stats = rank_stats(dist, coll if distributed else "cpu", distributed, kern_ms, launches, float(my_tasks.item()),
+                       elapsed)
     if distributed:
         tt = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
         all_reduce(tt, dist.ReduceOp.MAX)
@@ -235,7 +314,7 @@ def main():
     # verify every timed step against the golden tree
     tot = totals.cpu().numpy()
     tg, lg = GOLDEN.get(args.eps, (None, None))
-    ok = bool((tot[:, 3] == 0).all())
+    ok = bool((tot[:, 3] == 0).all()) and seen == world
     if tg is not None:
         ok = ok and bool((tot[:, 1] == tg).all() and (tot[:, 2] == lg).all())
     accepted_total = float(tot[:, 2].sum())
@@ -248,37 +327,8 @@ def main():
     achieved = FLOP_PER_TASK * tasks_per_launch / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
 
     if rank == 0:
-        out = {
-            "metric": "accepted subintervals/sec + FP64 F-evals/sec at 1/2/4/8 MI355X, EPSILON=1e-10",
-            "value": accepted_total / elapsed,
-            "unit": "accepted subintervals/s",
-            "f_evals_per_sec": f_evals / elapsed,
-            "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / K,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (analytic integrand, no dataset)",
-            "config": {"workload": "cosh4 on [0,5], EPSILON=%g (BASELINE %s); one step = a batch of %d "
-                                   "such integrals, each sharded over the GPUs"
-                                   % (args.eps, {1e-10: "configs[1]", 1e-12: "configs[4]"}.get(args.eps, "off-config"), B),
-                       "integrand": "cosh(x)^4 (aquadPartA.c:46)", "a": 0.0, "b": 5.0, "eps": args.eps,
-                       "tasks_per_integral": int(tot[0, 1]), "accepted_per_integral": int(tot[0, 2]),
-                       "parallelism": f"shard{world}" if world > 1 else "single-gpu",
-                       "integrals_per_step": B,
-                       "integrals_per_launch": per_launch,
-                       "workgroups_per_gpu": ctx.num_cus},
-            "single_integral_kernel_us": single_ms * 1e3 / single_n if single_n else None,
-            "verified": ok,
-            "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(tasks_per_launch),
-                         "kernel": "aq::k_stream<0,false,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
-                         "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": tasks_per_launch},
-            "cpu_baseline": cpu,
-        }
+        out = bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, per_launch, ctx.num_cus,
+                         single_ms, single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu)
         print(json.dumps(out))
     ctx.close()
     if distributed:

@@ -36,6 +36,8 @@
 
 namespace aq {
 
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
 #ifndef AQ_PT
 #define AQ_PT 768
 #endif
@@ -141,6 +143,26 @@ constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes bac
 #define AQ_PF_BELOW (WCAP / 4)
 #endif
 constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetches 64 cellar pairs
+// Lazy landing (r03). The prefetch used to be issued at <= PF_BELOW pairs and landed one round later,
+// inside a one-round burst: the landing's wait for the HBM loads (~2 us under load) stalled the wave
+// at nearly every cellar cycle (r03 A/B estimate: ~2.6 us per spill + prefetch, a fifth of the bench
+// launch). Now the loads go out at <= PF_ISSUE pairs, the bursts go on with them in flight, and they
+// land when the ring is down to <= PF_BELOW (a ring simulator of the bench's jobs, tools/ring_sim.py:
+// 80 % of the prefetches then have >= 2 rounds to arrive instead of 1). A ring that overflows while
+// they are in flight cancels them (the pairs are still in the cellar: only ctop moved) and spills.
+#ifndef AQ_PF_LAZY
+#define AQ_PF_LAZY 1
+#endif
+#ifndef AQ_PF_ISSUE
+#define AQ_PF_ISSUE 160   // r03 A/B (8192 x eps=1e-10): 96 -0.6 %, 128 -1.8 %, 160 -2.4 % vs landing after one round
+#endif
+constexpr bool PF_LAZY = AQ_PF_LAZY != 0;
+#ifndef AQ_OUTER_UNI
+#define AQ_OUTER_UNI 1
+#endif
+constexpr bool OUTER_UNI = AQ_OUTER_UNI != 0;   // re-assert the outer loop's wave state uniform (k_stream)
+constexpr int PF_ISSUE = PF_LAZY ? AQ_PF_ISSUE : AQ_PF_BELOW;
+static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
 #ifndef AQ_PREFETCH
 #define AQ_PREFETCH 1
 #endif
@@ -149,6 +171,9 @@ constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch
 #define AQ_SPILL 64   // r02 A/B: 128 at once 4.0 % slower at eps 1e-10, 6.5 % at 1e-12 (more refills)
 #endif
 constexpr int SPILL = AQ_SPILL;   // pairs a ring above WCAP - 64 moves to its cellar at once (a multiple of 64)
+#ifndef AQ_PIPE
+#define AQ_PIPE 0   // pipelined bursts: a round's pairs are read from the ring while the previous round evaluates
+#endif
 static_assert(SPILL % 64 == 0 && SPILL <= WCAP - 128, "spill whole lanes' worth, keep 64 pairs in the ring");
 
 struct alignas(128) Line {
@@ -244,10 +269,20 @@ struct Chunk {                      // SoA, one queue slot
 // the shared pool or seeds new work, so the cellar is empty whenever the wave reports idle. Only
 // the owning wave touches it; its lines are written back to HBM when the L2 evicts them (the PMC
 // passes measure ~13 GB of WRITE_SIZE per 8192-integral launch).
-struct Cellar {
-    double a[CCAP], b[CCAP], fa[CCAP], fm[CCAP], fb[CCAP];
-    unsigned dt[CCAP];
+//
+// Layout (r03): chunks of 64 pairs, each three 1-KiB planes {a, b} | {fa, fm} | {fb, dt word} of one
+// 16-B entry per pair -- the three f64x2 a pair's ds_read2st64 / ds_write2st64 move. A spill or a
+// refill of 64 pairs is then three LDS instructions and three global_*_dwordx4 from ONE address
+// each (one lane offset, the planes at +0 / +1 KiB / +2 KiB), where the SoA cellar of round 2 took
+// six LDS accesses at separate bases and six 64-bit addresses per side. The cellar top (ctop) only
+// ever moves by whole chunks (spills are SPILL pairs, prefetches and refills take whole chunks).
+struct CellarChunk {
+    f64x2 ab[64], ff[64], fd[64];
 };
+struct Cellar {
+    CellarChunk c[CCAP / 64];
+};
+static_assert(CCAP % 64 == 0, "the cellar moves whole 64-pair chunks");
 
 // Launch-to-launch job-size hint (one per context): every workgroup adds the tasks it ran, the last
 // one to exit turns the mean per integral into the next adaptive launch's shares per integral
@@ -442,7 +477,6 @@ __device__ __forceinline__ double2 sload_bounds(const double2* base, int p) {
 // LDS operations it does not see -- and the "memory" clobbers keep the compiler's own LDS accesses
 // on their side of both.
 static_assert(LREC * 8 == 50 * 512, "lds_pop6 / lds_push6 assume 50 x 512 B per field");
-typedef double f64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void lds_pop6(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
                                          unsigned& dt) {
     f64x2 ab, ff, fd;
@@ -467,6 +501,45 @@ __device__ __forceinline__ void lds_push6(unsigned addr, double a, double b, dou
         :
         : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb), "v"(dw)
         : "memory");
+}
+// The pipelined burst's pair registers: one slot's six fields as lds_pop6 reads them, in two steps.
+// lds_issue6 only ISSUES the three ds_read2st64_b64; lds_wait6 waits for every outstanding LDS access
+// and is the point from which the registers hold the pair -- nothing may read them before (the
+// hardware does not interlock a register an LDS load is still writing). The caller calls lds_wait6
+// late in the same round, after the compiler's own waits for the exp-table reads issued after these
+// loads: LDS accesses of one wave complete in order, so by then the wait costs nothing.
+struct PairRegs {
+    f64x2 ab, ff, fd;   // {a, b}, {fa, fm}, {fb, dt word}
+};
+__device__ __forceinline__ void lds_issue6(unsigned addr, PairRegs& r) {
+    asm volatile(
+        "ds_read2st64_b64 %0, %3 offset1:50\n\t"
+        "ds_read2st64_b64 %1, %3 offset0:100 offset1:150\n\t"
+        "ds_read2st64_b64 %2, %3 offset0:200 offset1:250"
+        : "=&v"(r.ab), "=&v"(r.ff), "=&v"(r.fd)
+        : "v"(addr)
+        : "memory");
+}
+__device__ __forceinline__ void lds_wait6(PairRegs& r) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.ab), "+v"(r.ff), "+v"(r.fd) : : "memory");
+}
+__device__ __forceinline__ void lds_store6(unsigned addr, const PairRegs& r) {
+    asm volatile(
+        "ds_write2st64_b64 %0, %1, %2 offset1:50\n\t"
+        "ds_write2st64_b64 %0, %3, %4 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %0, %5, %6 offset0:200 offset1:250"
+        :
+        : "v"(addr), "v"(r.ab.x), "v"(r.ab.y), "v"(r.ff.x), "v"(r.ff.y), "v"(r.fd.x), "v"(r.fd.y)
+        : "memory");
+}
+// one lane's pair of a cellar chunk (three global_load_dwordx4 / global_store_dwordx4)
+__device__ __forceinline__ PairRegs chunk_load(const CellarChunk* ch, unsigned lane) {
+    return PairRegs{ch->ab[lane], ch->ff[lane], ch->fd[lane]};
+}
+__device__ __forceinline__ void chunk_store(CellarChunk* ch, unsigned lane, const PairRegs& r) {
+    ch->ab[lane] = r.ab;
+    ch->ff[lane] = r.ff;
+    ch->fd[lane] = r.fd;
 }
 // LDS byte address of ring index i of a wave's ring at byte offset ring8 (a multiple of WCAP * 8):
 // one shift-add and one and-or. vmask = (WCAP - 1) << 3 held in a VGPR (a gfx9 VOP3 reads one
@@ -610,8 +683,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // cellar prefetch in flight: up to 64 pairs, one per lane, landed below the ring's bottom at
     // the top of the next iteration (the loads overlap one round)
     unsigned pf_n = 0;
-    double pf_a = 0, pf_b = 0, pf_fa = 0, pf_fm = 0, pf_fb = 0;
-    unsigned pf_dt = 0;
+    PairRegs pf{};
     unsigned long long cl0 = 0;
     if constexpr (DIAG) {
         if (tid == 0) s_dg[DG_T_START] = t_entry;
@@ -620,17 +692,23 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
     const ExpConsts kk = pinned_exp_consts();
     for (;;) {
-        if (pf_n) {
+        // the wave's ring / cellar state, re-asserted uniform once per iteration: the loop's many
+        // divergent lane-level blocks (copies, seeding) otherwise leave it in VGPRs, and every check
+        // below becomes a v_cmp + exec-mask branch instead of a scalar compare
+        if constexpr (OUTER_UNI) {
+            top = uni(top);
+            bot = uni(bot);
+            ctop = uni(ctop);
+            pf_n = uni(pf_n);
+            poll_ctr = uni(poll_ctr);
+        }
+        if (pf_n && (!PF_LAZY || top - bot <= (unsigned)PF_BELOW)) {
             if (bot < 64u) {   // keep ring indices non-negative (slots are index % WCAP)
                 bot += (unsigned)WCAP;
                 top += (unsigned)WCAP;
             }
             bot -= pf_n;
-            if (lane < pf_n) {
-                const unsigned j = base + ring_slot(bot + lane);
-                s_a[j] = pf_a; s_b[j] = pf_b; s_fa[j] = pf_fa; s_fm[j] = pf_fm; s_fb[j] = pf_fb;
-                s_dt[j] = pf_dt;
-            }
+            if (lane < pf_n) lds_store6(ring_addr(ring8, ring_slot(bot) + lane, ring_vmask), pf);
             __builtin_amdgcn_wave_barrier();   // reconverge here: the ring indices stay wave-uniform
             pf_n = 0;
         }
@@ -641,15 +719,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (ctop > 0) {
                 unsigned long long cr = 0;
                 if constexpr (DIAG) cr = clk();
-                const unsigned k = min(ctop, (unsigned)REFILL), c0 = ctop - k;
+                const unsigned k = min(ctop, (unsigned)REFILL), c0 = ctop - k;   // whole chunks
                 // no wait for this wave's own spills: one wave's accesses to one address stay in
                 // order, and only this wave ever touches its cellar
-                for (unsigned q = lane; q < k; q += 64) {
-                    const unsigned i = c0 + q, j = base + q;
-                    s_a[j] = cel->a[i]; s_b[j] = cel->b[i];
-                    s_fa[j] = cel->fa[i]; s_fm[j] = cel->fm[i]; s_fb[j] = cel->fb[i];
-                    s_dt[j] = cel->dt[i];
-                }
+                for (unsigned q = 0; q < k; q += 64)
+                    lds_store6(ring_addr(ring8, q + lane, ring_vmask), chunk_load(&cel->c[(c0 + q) / 64u], lane));
                 ctop = c0;
                 bot = 0;
                 top = k;
@@ -1104,12 +1178,19 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // ---- keep the ring from overflowing: its bottom 64 pairs go to the cellar, else the pool,
         //      else an HBM chunk
         if (size > (unsigned)(WCAP - 64)) {
+            if (PF_LAZY && pf_n) {
+                // a prefetch in flight is cancelled: its pairs never left the cellar (the loads land in
+                // registers nobody reads; the next spill writes above them)
+                ctop += pf_n;
+                pf_n = 0;
+            }
             if (ctop + (unsigned)SPILL <= (unsigned)CCAP) {
 #pragma unroll
                 for (unsigned q = 0; q < (unsigned)SPILL; q += 64u) {
-                    const unsigned i = ctop + q + lane, j = base + ring_slot(bot + q + lane);
-                    cel->a[i] = s_a[j]; cel->b[i] = s_b[j];
-                    cel->fa[i] = s_fa[j]; cel->fm[i] = s_fm[j]; cel->fb[i] = s_fb[j]; cel->dt[i] = s_dt[j];
+                    PairRegs r;
+                    lds_issue6(ring_addr(ring8, ring_slot(bot + q) + lane, ring_vmask), r);
+                    lds_wait6(r);
+                    chunk_store(&cel->c[(ctop + q) / 64u], lane, r);
                 }
                 ctop += (unsigned)SPILL;
                 bot += (unsigned)SPILL;
@@ -1220,15 +1301,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
 
         // ---- running low: fetch the next 64 cellar pairs now, land them next iteration
-        if (PREFETCH && ctop > 0 && size <= (unsigned)PF_BELOW) {
-            pf_n = min(ctop, 64u);
+        if (PREFETCH && ctop > 0 && pf_n == 0 && size <= (unsigned)PF_ISSUE) {
+            pf_n = 64u;   // ctop is a whole number of chunks
             ctop -= pf_n;
-            if (lane < pf_n) {   // (same-wave, same-address order: no wait for the spills)
-                const unsigned i = ctop + lane;
-                pf_a = cel->a[i]; pf_b = cel->b[i];
-                pf_fa = cel->fa[i]; pf_fm = cel->fm[i]; pf_fb = cel->fb[i];
-                pf_dt = cel->dt[i];
-            }
+            // (same-wave, same-address order: no wait for the spills)
+            pf = chunk_load(&cel->c[ctop / 64u], lane);
             __builtin_amdgcn_wave_barrier();
             if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }
         }
@@ -1249,10 +1326,134 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // lo = PF_BELOW while the cellar holds pairs to prefetch (else 0: stop when empty), hi =
         // WCAP - 64 (near overflow), or hi = lo while a prefetch is in flight (one round only).
         // One subtract and one compare per round, and one compare for the round counter.
-        const unsigned b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
-        const unsigned b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
+        unsigned b_lo1, b_span;
+        if constexpr (PF_LAZY) {
+            // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar holds
+            // pairs and none is (issue one), else 0 (stop when empty); hi = WCAP - 64
+            b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_ISSUE : 0u)) + 1u;
+            b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
+        } else {
+            b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
+            b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
+        }
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
         unsigned b_r = 0;                                              // rounds run in this burst
+#if AQ_PIPE
+        // Pipelined burst. Round r reads the pairs of round r + 1 (nxt) from the ring top as it starts
+        // and evaluates its own (cur, read by round r - 1), so the ring's LDS latency hides behind the
+        // F chains instead of opening every round. Its children then go over the slots nxt came from:
+        // one wave's LDS accesses complete in order, so those reads return the old pairs. The ring
+        // indices exclude cur and nxt; the size window counts them. Two register sets alternate
+        // (the loop is unrolled by two: no copies), and nxt goes back on top when the burst ends.
+        PairRegs rs1, rs2;
+        unsigned n1 = min(b_size, 64u), n2 = 0;
+        b_top -= n1;
+        lds_issue6(ring_addr(ring8, ring_slot(b_top) + lane, ring_vmask), rs1);
+        lds_wait6(rs1);
+        auto round = [&](PairRegs& cur, const unsigned n, PairRegs& nxt, unsigned& nn) -> bool {
+            unsigned long long c0 = 0, c1 = 0;
+            if constexpr (DIAG) c0 = clk();
+            nn = min(b_top - b_bot, 64u);                       // nxt: the ring's top nn pairs
+            const unsigned b0 = b_top - nn;
+            const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
+            // every lane reads a slot (lanes >= nn a stale, harmless one): no per-lane defaults
+            lds_issue6(ring_addr(ring8, b0s + lane, ring_vmask), nxt);
+            const bool act = lane < n;
+            const double pa = cur.ab.x, pb = cur.ab.y, pfa = cur.ff.x, pfm = cur.ff.y, pfb = cur.fd.x;
+            const unsigned dt = (unsigned)__double_as_longlong(cur.fd.y);
+                Step2 st[2];
+                // both midpoints lie in [pa, pb]: one range test for the pair
+                // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
+                // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
+                // compiler turns the byte test into an and plus a compare
+                unsigned long long nospan = 0ull;
+                if constexpr (FID == F_COSH4)
+                    asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
+                // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
+                // measured 0.9 % slower)
+                const unsigned long long am = __ballot(act);
+                // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
+                double pm, hm;
+                pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+                lds_wait6(nxt);   // (after the step's exp-table waits, which the nxt loads precede)
+                // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
+                // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
+                // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
+                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+                const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
+                const unsigned long long okm = am & dm;
+                // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
+                const unsigned long long atcap = am & ~dm;
+                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
+                // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
+                // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
+                // counts are wave-level, the area one masked add per accepted task.
+                const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
+                b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
+                // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
+                // (doubled areas: halved at flush); the deepest pair popped, under the active mask
+                masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, dt, am);
+                if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
+                                        // takes and seeds switch the tag); checked in diagnostic builds
+                    const int rtag = (int)(dt >> TAG_SHIFT);
+                    b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
+                }
+                if (HIST) {
+                    const unsigned d = dt & 255u;
+                    if (__builtin_amdgcn_inverse_ballot_w64(am)) {
+                        atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                        const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
+                        if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+                    }
+                }
+                if constexpr (DIAG) c1 = clk();
+                // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
+                // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
+                const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
+                const unsigned cnt0 = (unsigned)__popcll(mask0);
+                const unsigned cdt = dt + 1u;                       // depth + 1, same integral
+                if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
+                    lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
+                }
+                if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
+                    lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
+                }
+                b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
+                if constexpr (DIAG) {
+                    if (lane == 0) {
+                        const unsigned long long c2 = clk();
+                        atomicAdd(&s_dg[DG_ROUNDS], 1ull);
+                        atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
+                        atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
+                        atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
+                        atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
+                        atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
+                    }
+                    const unsigned nt = 2u * n;
+                    if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
+                }
+                const unsigned sz = b_top - b_bot + nn;             // the ring with nxt
+                b_size = sz;
+                ++b_r;
+                // one compare: the give / poll round closes the size window (opaque, so the compiler
+                // does not split it back into two conditions joined by SALU selects)
+                unsigned span_r = b_r != b_max ? b_span : 0u;
+                asm("" : "+s"(span_r));
+                __builtin_amdgcn_wave_barrier();
+                return sz - b_lo1 < span_r;
+            };
+        // nxt back on top of the ring (none when the ring ran empty)
+        auto put_back = [&](PairRegs& r, unsigned nn) {
+            if (lane < nn)
+                lds_push6(ring_addr(ring8, ring_slot(b_top) + lane, ring_vmask), r.ab.x, r.ab.y, r.ff.x, r.ff.y,
+                          r.fd.x, (unsigned)__double_as_longlong(r.fd.y));
+            b_top += nn;
+        };
+        for (;;) {
+            if (!round(rs1, n1, rs2, n2)) { put_back(rs2, n2); break; }
+            if (!round(rs2, n2, rs1, n1)) { put_back(rs1, n1); break; }
+        }
+#else
         bool b_go;
         do {
             // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
@@ -1347,6 +1548,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             b_go = sz - b_lo1 < span_r;
             __builtin_amdgcn_wave_barrier();
         } while (b_go);
+#endif
         b_poll += b_r - 1u;   // every round but the burst's last advances the give / poll counter
         top = b_top;
         poll_ctr = b_poll;
