@@ -160,7 +160,15 @@ constexpr bool PF_LAZY = AQ_PF_LAZY != 0;
 #ifndef AQ_OUTER_UNI
 #define AQ_OUTER_UNI 1
 #endif
-constexpr bool OUTER_UNI = AQ_OUTER_UNI != 0;   // re-assert the outer loop's wave state uniform (k_stream)
+constexpr bool OUTER_UNI = AQ_OUTER_UNI != 0;
+// In-burst cellar moves (r03): a round that leaves the burst's size window at a cellar edge -- above
+// the spill line, or down to the prefetch issue / landing line -- moves the chunk inside the burst
+// and the burst goes on, where round 2 left the burst for the outer loop (~60 VALU and ~70 SALU of
+// re-checks and state moves per exit, 0.24 exits per round: tools/ring_sim.py, PMC r03e).
+#ifndef AQ_INBURST
+#define AQ_INBURST 1
+#endif
+constexpr bool INBURST = AQ_INBURST != 0;   // re-assert the outer loop's wave state uniform (k_stream)
 constexpr int PF_ISSUE = PF_LAZY ? AQ_PF_ISSUE : AQ_PF_BELOW;
 static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
 #ifndef AQ_PREFETCH
@@ -171,9 +179,6 @@ constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch
 #define AQ_SPILL 64   // r02 A/B: 128 at once 4.0 % slower at eps 1e-10, 6.5 % at 1e-12 (more refills)
 #endif
 constexpr int SPILL = AQ_SPILL;   // pairs a ring above WCAP - 64 moves to its cellar at once (a multiple of 64)
-#ifndef AQ_PIPE
-#define AQ_PIPE 0   // pipelined bursts: a round's pairs are read from the ring while the previous round evaluates
-#endif
 static_assert(SPILL % 64 == 0 && SPILL <= WCAP - 128, "spill whole lanes' worth, keep 64 pairs in the ring");
 
 struct alignas(128) Line {
@@ -690,6 +695,16 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         cl0 = clk();
     }
 
+    // the ring's bottom SPILL pairs (ring index b) to the cellar's chunks from pair c (whole chunks)
+    auto spill_to_cellar = [&](unsigned b, unsigned c) {
+        for (unsigned q = 0; q < (unsigned)SPILL; q += 64u) {
+            PairRegs r;
+            lds_issue6(ring_addr(ring8, ring_slot(b + q) + lane, ring_vmask), r);
+            lds_wait6(r);
+            chunk_store(&cel->c[(c + q) / 64u], lane, r);
+        }
+        if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
+    };
     const ExpConsts kk = pinned_exp_consts();
     for (;;) {
         // the wave's ring / cellar state, re-asserted uniform once per iteration: the loop's many
@@ -1185,16 +1200,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 pf_n = 0;
             }
             if (ctop + (unsigned)SPILL <= (unsigned)CCAP) {
-#pragma unroll
-                for (unsigned q = 0; q < (unsigned)SPILL; q += 64u) {
-                    PairRegs r;
-                    lds_issue6(ring_addr(ring8, ring_slot(bot + q) + lane, ring_vmask), r);
-                    lds_wait6(r);
-                    chunk_store(&cel->c[(ctop + q) / 64u], lane, r);
-                }
+                spill_to_cellar(bot, ctop);
                 ctop += (unsigned)SPILL;
                 bot += (unsigned)SPILL;
-                if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
@@ -1320,140 +1328,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned b_top0 = b_top;
         unsigned b_n = 0;                 // pairs popped in this burst (2 tasks each)
         unsigned long long b_dv = 0;      // lanes that met the depth cap with a refining task
-        const unsigned b_bot = uni(bot), b_ctop = uni(ctop), b_pf = uni(pf_n);
+        unsigned b_bot = uni(bot), b_ctop = uni(ctop), b_pf = uni(pf_n);
         bool b_mixed = uni(mixed);
         // the burst goes on while lo < size <= hi and the next round is no give / poll round:
         // lo = PF_BELOW while the cellar holds pairs to prefetch (else 0: stop when empty), hi =
         // WCAP - 64 (near overflow), or hi = lo while a prefetch is in flight (one round only).
         // One subtract and one compare per round, and one compare for the round counter.
         unsigned b_lo1, b_span;
-        if constexpr (PF_LAZY) {
-            // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar holds
-            // pairs and none is (issue one), else 0 (stop when empty); hi = WCAP - 64
-            b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_ISSUE : 0u)) + 1u;
-            b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
-        } else {
-            b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
-            b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
-        }
+        auto window = [&]() {
+            if constexpr (PF_LAZY) {
+                // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar
+                // holds pairs and none is (issue one), else 0 (stop when empty); hi = WCAP - 64
+                b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_ISSUE : 0u)) + 1u;
+                b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
+            } else {
+                b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
+                b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
+            }
+        };
+        window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
         unsigned b_r = 0;                                              // rounds run in this burst
-#if AQ_PIPE
-        // Pipelined burst. Round r reads the pairs of round r + 1 (nxt) from the ring top as it starts
-        // and evaluates its own (cur, read by round r - 1), so the ring's LDS latency hides behind the
-        // F chains instead of opening every round. Its children then go over the slots nxt came from:
-        // one wave's LDS accesses complete in order, so those reads return the old pairs. The ring
-        // indices exclude cur and nxt; the size window counts them. Two register sets alternate
-        // (the loop is unrolled by two: no copies), and nxt goes back on top when the burst ends.
-        PairRegs rs1, rs2;
-        unsigned n1 = min(b_size, 64u), n2 = 0;
-        b_top -= n1;
-        lds_issue6(ring_addr(ring8, ring_slot(b_top) + lane, ring_vmask), rs1);
-        lds_wait6(rs1);
-        auto round = [&](PairRegs& cur, const unsigned n, PairRegs& nxt, unsigned& nn) -> bool {
-            unsigned long long c0 = 0, c1 = 0;
-            if constexpr (DIAG) c0 = clk();
-            nn = min(b_top - b_bot, 64u);                       // nxt: the ring's top nn pairs
-            const unsigned b0 = b_top - nn;
-            const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
-            // every lane reads a slot (lanes >= nn a stale, harmless one): no per-lane defaults
-            lds_issue6(ring_addr(ring8, b0s + lane, ring_vmask), nxt);
-            const bool act = lane < n;
-            const double pa = cur.ab.x, pb = cur.ab.y, pfa = cur.ff.x, pfm = cur.ff.y, pfb = cur.fd.x;
-            const unsigned dt = (unsigned)__double_as_longlong(cur.fd.y);
-                Step2 st[2];
-                // both midpoints lie in [pa, pb]: one range test for the pair
-                // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
-                // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
-                // compiler turns the byte test into an and plus a compare
-                unsigned long long nospan = 0ull;
-                if constexpr (FID == F_COSH4)
-                    asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
-                // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
-                // measured 0.9 % slower)
-                const unsigned long long am = __ballot(act);
-                // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
-                double pm, hm;
-                pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
-                lds_wait6(nxt);   // (after the step's exp-table waits, which the nxt loads precede)
-                // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
-                // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
-                // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
-                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
-                const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
-                const unsigned long long okm = am & dm;
-                // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
-                const unsigned long long atcap = am & ~dm;
-                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
-                // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
-                // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
-                // counts are wave-level, the area one masked add per accepted task.
-                const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
-                b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
-                // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-                // (doubled areas: halved at flush); the deepest pair popped, under the active mask
-                masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, dt, am);
-                if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
-                                        // takes and seeds switch the tag); checked in diagnostic builds
-                    const int rtag = (int)(dt >> TAG_SHIFT);
-                    b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
-                }
-                if (HIST) {
-                    const unsigned d = dt & 255u;
-                    if (__builtin_amdgcn_inverse_ballot_w64(am)) {
-                        atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
-                        const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
-                        if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
-                    }
-                }
-                if constexpr (DIAG) c1 = clk();
-                // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
-                // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
-                const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-                const unsigned cnt0 = (unsigned)__popcll(mask0);
-                const unsigned cdt = dt + 1u;                       // depth + 1, same integral
-                if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
-                    lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
-                }
-                if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
-                    lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
-                }
-                b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
-                if constexpr (DIAG) {
-                    if (lane == 0) {
-                        const unsigned long long c2 = clk();
-                        atomicAdd(&s_dg[DG_ROUNDS], 1ull);
-                        atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
-                        atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
-                        atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
-                        atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
-                        atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
-                    }
-                    const unsigned nt = 2u * n;
-                    if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
-                }
-                const unsigned sz = b_top - b_bot + nn;             // the ring with nxt
-                b_size = sz;
-                ++b_r;
-                // one compare: the give / poll round closes the size window (opaque, so the compiler
-                // does not split it back into two conditions joined by SALU selects)
-                unsigned span_r = b_r != b_max ? b_span : 0u;
-                asm("" : "+s"(span_r));
-                __builtin_amdgcn_wave_barrier();
-                return sz - b_lo1 < span_r;
-            };
-        // nxt back on top of the ring (none when the ring ran empty)
-        auto put_back = [&](PairRegs& r, unsigned nn) {
-            if (lane < nn)
-                lds_push6(ring_addr(ring8, ring_slot(b_top) + lane, ring_vmask), r.ab.x, r.ab.y, r.ff.x, r.ff.y,
-                          r.fd.x, (unsigned)__double_as_longlong(r.fd.y));
-            b_top += nn;
-        };
-        for (;;) {
-            if (!round(rs1, n1, rs2, n2)) { put_back(rs2, n2); break; }
-            if (!round(rs2, n2, rs1, n1)) { put_back(rs1, n1); break; }
-        }
-#else
         bool b_go;
         do {
             // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
@@ -1546,9 +1441,46 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             unsigned span_r = b_r != b_max ? b_span : 0u;
             asm("" : "+s"(span_r));
             b_go = sz - b_lo1 < span_r;
+            if (INBURST && PF_LAZY && __builtin_expect(!b_go, 0) && b_r != b_max && sz != 0u) {
+                // a cellar edge (not the give / poll round, not an empty ring): move the chunk here
+                // and go on (the cellar-full spill and the pool / queue fallbacks stay outside)
+                if (sz > (unsigned)(WCAP - 64)) {
+                    if (b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
+                        if (b_pf) {   // cancel the prefetch in flight (its pairs never left the cellar)
+                            b_ctop += b_pf;
+                            b_pf = 0;
+                        }
+                        spill_to_cellar(b_bot, b_ctop);
+                        b_ctop += (unsigned)SPILL;
+                        b_bot += (unsigned)SPILL;
+                        b_go = true;
+                    }
+                } else if (b_pf) {                   // down to PF_BELOW: land the prefetch
+                    if (b_bot < 64u) {
+                        b_bot += (unsigned)WCAP;
+                        b_top += (unsigned)WCAP;
+                    }
+                    b_bot -= b_pf;
+                    if (lane < b_pf) lds_store6(ring_addr(ring8, ring_slot(b_bot) + lane, ring_vmask), pf);
+                    b_pf = 0;
+                    b_go = true;
+                } else if (PREFETCH && b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
+                    b_pf = 64u;
+                    b_ctop -= 64u;
+                    pf = chunk_load(&cel->c[b_ctop / 64u], lane);
+                    if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], 64ull); }
+                    b_go = true;
+                }
+                if (b_go) {
+                    window();
+                    b_size = b_top - b_bot;
+                }
+            }
             __builtin_amdgcn_wave_barrier();
         } while (b_go);
-#endif
+        bot = b_bot;
+        ctop = b_ctop;
+        pf_n = b_pf;
         b_poll += b_r - 1u;   // every round but the burst's last advances the give / poll counter
         top = b_top;
         poll_ctr = b_poll;

@@ -8,6 +8,8 @@ import os
 import sys
 
 root = sys.argv[1]
+WAVES_PER_SIMD = 3   # k_stream: 12 waves per workgroup, one workgroup per CU, 4 SIMDs
+TASKS = float(os.environ.get("PMC_TASKS", 8192 * 1464273))   # tasks per dispatch (tools/pmc_profile.sh's launch)
 out = {}
 for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
     eng = os.path.basename(os.path.dirname(f))
@@ -23,7 +25,25 @@ for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
     big = sorted(per.items(), key=lambda kv: -max(kv[1].values()))[:2]
     avg = {k: sum(d[1].get(k, 0) for d in big) / len(big) for k in big[0][1]}
     if "SQ_ACTIVE_INST_VALU" in avg and avg.get("SQ_WAVE_CYCLES"):
-        avg["valu_busy_frac_per_simd_est"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+        # SQ_WAVE_CYCLES and SQ_ACTIVE_INST_VALU are both summed over every wave (quad-cycles): their
+        # ratio is the share of a WAVE's time in which it issues VALU. The persistent kernel keeps
+        # WAVES_PER_SIMD (3) waves resident on every SIMD for the whole dispatch, so the SIMD's VALU
+        # busy share is that ratio times 3 (the r02 tool reported the per-wave ratio as per-SIMD).
+        avg["valu_issue_frac_per_wave"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+        avg["valu_busy_frac_per_simd_est"] = WAVES_PER_SIMD * avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+    if avg.get("SQ_WAVE_CYCLES"):
+        for k in ("SQ_WAIT_INST_LDS", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                  "SQ_ACTIVE_INST_ANY"):
+            if k in avg:
+                avg[k.lower() + "_share_of_wave_cycles"] = avg[k] / avg["SQ_WAVE_CYCLES"]
+    if TASKS:
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_VALU_INT32"):
+            if k in avg:
+                avg[k.lower() + "_per_task"] = avg[k] / TASKS
+        f64 = sum(avg.get(k, 0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+        if f64:
+            avg["fp64_insts_per_task"] = f64 / TASKS
     out[eng] = {"kernel": names[big[0][0]][:60], "dispatches": [d[0] for d in big], "avg": avg}
 print(json.dumps(out, indent=1))
 
