@@ -131,7 +131,7 @@ def rank_stats(dist, coll, distributed, kern_ms, launches, tasks, elapsed):
 
 
 def bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, per_launch, ctx_cus, single_ms,
-               single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu):
+               single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu, cu_stats=None):
     """The one JSON line rank 0 prints (the driver's contract plus roofline, cpu_baseline and the
     multi-rank fields: backend, ranks_seen -- counted by a collective -- and per-rank kernel time and
     tasks with their imbalance)."""
@@ -163,6 +163,7 @@ def bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, 
         "backend": backend,
         "ranks_seen": seen,
         "per_rank": stats,
+        "tasks_per_cu": cu_stats,
         "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(tasks_per_launch),
                      "kernel": "aq::k_stream<0,false,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
@@ -276,6 +277,7 @@ def main():
         w += m
     ctx.synchronize()
 
+    ctx.cu_task_counters(reset=True)   # per-CU task counters over the timed launches only
     K = args.steps
     n_int = K * B
     totals = torch.zeros((n_int, 4), dtype=torch.float64, device="cuda")
@@ -311,10 +313,17 @@ def main():
         kern_avg_ms = kern_ms / max(launches, 1)
     per_launch = n_int / max(launches, 1)
 
+    # this rank's tasks per CU over the timed launches (every launch shape keeps them: aq_cu_task_counters)
+    cu = ctx.cu_task_counters(reset=True)
+    cu_v = list(cu.values())
+    cu_stats = {"n_cu": len(cu_v), "min": min(cu_v) if cu_v else 0, "max": max(cu_v) if cu_v else 0,
+                "imbalance": (max(cu_v) * len(cu_v) / sum(cu_v)) if cu_v and sum(cu_v) else None,
+                "sum": sum(cu_v)}
+
     # verify every timed step against the golden tree
     tot = totals.cpu().numpy()
     tg, lg = GOLDEN.get(args.eps, (None, None))
-    ok = bool((tot[:, 3] == 0).all()) and seen == world
+    ok = bool((tot[:, 3] == 0).all()) and seen == world and cu_stats["sum"] == int(my_tasks.item())
     if tg is not None:
         ok = ok and bool((tot[:, 1] == tg).all() and (tot[:, 2] == lg).all())
     accepted_total = float(tot[:, 2].sum())
@@ -328,7 +337,8 @@ def main():
 
     if rank == 0:
         out = bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, per_launch, ctx.num_cus,
-                         single_ms, single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu)
+                         single_ms, single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu,
+                         cu_stats)
         print(json.dumps(out))
     ctx.close()
     if distributed:

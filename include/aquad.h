@@ -198,12 +198,26 @@ int aq_level_step_chained(aq_ctx *ctx, int integrand, const double *d_in, const 
                           double *d_out, uint32_t cap_out, double eps, int depth, int max_depth, uint32_t *d_n_out,
                           double *d_acc);
 
+/* `levels` consecutive levels in ONE single-workgroup launch (the narrow top of the tree, where a
+ * launch per level is launch- and latency-bound): level depth + k reads d_counts[depth + k] records
+ * from d_buf{k & 1} and appends its children to d_buf{(k + 1) & 1} (at most cap records), writing
+ * their number to d_counts[depth + k + 1]; the accepted areas and counts add into d_acc as
+ * aq_level_step's do. The last level's children are in d_buf{levels & 1}. Asynchronous. */
+int aq_level_narrow(aq_ctx *ctx, int integrand, double *d_buf0, double *d_buf1, uint32_t cap, uint32_t *d_counts,
+                    int depth, int levels, double eps, int max_depth, double *d_acc);
+
 /* Per-level task / accepted histograms of the last aq_integrate* call (levels 0..maxlev-1). */
 int aq_level_histogram(aq_ctx *ctx, uint64_t *tasks_per_level, uint64_t *leaves_per_level, int maxlev);
 
 /* Per-CU task counters of the last call (tasks_per_process[] mapped to compute units).
  * out[AQ_CU_SLOTS] indexed by hardware slot; returns the number of non-zero slots. */
 int aq_tasks_per_cu(aq_ctx *ctx, uint64_t *out, int cap);
+/* Per-CU task counters of EVERY persistent launch (any shape: lone integrals, batches, shards),
+ * summed since the context was created or last reset: each workgroup adds its tasks to its hardware
+ * CU slot once at exit. out[AQ_CU_SLOTS] by hardware slot (cap entries written); reset != 0 zeroes
+ * the counters after the read. Waits for the context's stream. Returns the number of non-zero slots.
+ * Σ out == Σ tasks of the launches since the reset (every task is counted by the CU that ran it). */
+int aq_cu_task_counters(aq_ctx *ctx, uint64_t *out, int cap, int reset);
 
 /* Batch front end (SURVEY config 3): n independent integrals [a[i], b[i]] of one integrand.
  * Per-integral area / accepted / tasks (any may be NULL). NOTE the output order: accepted BEFORE

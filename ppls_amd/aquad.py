@@ -265,6 +265,15 @@ class Context:
             _check(n, "aq_diagnostics")
         return out[:w * n].reshape(n, w), self.DIAG_FIELDS
 
+    def cu_task_counters(self, reset: bool = False) -> Dict[int, int]:
+        """Tasks per hardware CU slot over every persistent launch since the last reset (any launch
+        shape: the farmer's tasks_per_process, aquadPartA.c:162, per CU). Waits for the stream."""
+        cu = np.zeros(_lib.AQ_CU_SLOTS, np.uint64)
+        n = self.L.aq_cu_task_counters(self._h, _up(cu), _lib.AQ_CU_SLOTS, 1 if reset else 0)
+        if n < 0:
+            _check(n, "aq_cu_task_counters")
+        return {int(i): int(cu[i]) for i in np.nonzero(cu)[0]}
+
     # -- batch / libm ------------------------------------------------------------------------
     def integrate_batch(self, a, b, eps, integrand=COSH4):
         a = np.ascontiguousarray(a, np.float64)

@@ -165,6 +165,12 @@ constexpr bool OUTER_UNI = AQ_OUTER_UNI != 0;
 // the spill line, or down to the prefetch issue / landing line -- moves the chunk inside the burst
 // and the burst goes on, where round 2 left the burst for the outer loop (~60 VALU and ~70 SALU of
 // re-checks and state moves per exit, 0.24 exits per round: tools/ring_sim.py, PMC r03e).
+#ifndef AQ_PREBURST_WAIT
+#define AQ_PREBURST_WAIT 0   // r03 A/B: no effect
+#endif
+#ifndef AQ_INB_MASK
+#define AQ_INB_MASK 7
+#endif
 #ifndef AQ_INBURST
 #define AQ_INBURST 1
 #endif
@@ -319,6 +325,8 @@ struct StreamParams {
     QCtl* q_next;                   // the next launch's: workgroup 0 zeroes it
     unsigned long long* parts;      // [2 * (slot * gridDim.x + wg) + 0/1]: per-CU launches' counts (slot_counts)
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
+    unsigned long long* cu_acc;     // [AQ_CU_SLOTS] tasks per hardware CU slot, summed over launches
+                                    // (every launch: the farmer's tasks_per_process, :162, per CU)
     Chunk* chunks;
     Cellar* cellar;                 // [gridDim.x * NW]
     unsigned* ready;
@@ -1350,6 +1358,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
         unsigned b_r = 0;                                              // rounds run in this burst
         bool b_go;
+#if AQ_PREBURST_WAIT
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), compiler-visible: nothing pending at the burst's header
+#endif
         do {
             // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
             //      tasks of a pair are evaluated together (two interleaved cosh chains)
@@ -1445,7 +1456,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // a cellar edge (not the give / poll round, not an empty ring): move the chunk here
                 // and go on (the cellar-full spill and the pool / queue fallbacks stay outside)
                 if (sz > (unsigned)(WCAP - 64)) {
-                    if (b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
+                    if ((AQ_INB_MASK & 1) && b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
                         if (b_pf) {   // cancel the prefetch in flight (its pairs never left the cellar)
                             b_ctop += b_pf;
                             b_pf = 0;
@@ -1455,7 +1466,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         b_bot += (unsigned)SPILL;
                         b_go = true;
                     }
-                } else if (b_pf) {                   // down to PF_BELOW: land the prefetch
+                } else if ((AQ_INB_MASK & 2) && b_pf) {                   // down to PF_BELOW: land the prefetch
                     if (b_bot < 64u) {
                         b_bot += (unsigned)WCAP;
                         b_top += (unsigned)WCAP;
@@ -1464,7 +1475,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if (lane < b_pf) lds_store6(ring_addr(ring8, ring_slot(b_bot) + lane, ring_vmask), pf);
                     b_pf = 0;
                     b_go = true;
-                } else if (PREFETCH && b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
+                } else if ((AQ_INB_MASK & 4) && PREFETCH && b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
                     b_pf = 64u;
                     b_ctop -= 64u;
                     pf = chunk_load(&cel->c[b_ctop / 64u], lane);
@@ -1514,13 +1525,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
         // job-size hint for the next adaptive launch: the last wave of each workgroup adds the
         // workgroup's tasks, the last workgroup sets shares per integral for ~TASKS_PER_JOB per job
-        bool last = false;
-        if (PCU || (P.adaptive & 2)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's LDS flushes precede its exit count
-            last = atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
+        // (every launch: the workgroup's tasks also go to the context's per-CU counters, below)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's LDS flushes precede its exit count
+        const bool last = atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         last_u = last ? 1u : 0u;
+        if (last) {
+            // per-CU task counters on every launch shape: the workgroup's tasks, once,
+            // into its hardware CU slot -- one atomic per workgroup and launch, on 256 distinct lines
+            const unsigned long long wt = __hip_atomic_load(&S.tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (wt) __hip_atomic_fetch_add(&P.cu_acc[cu_slot()], wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if constexpr (DIAG) { if (last) atomicMax(&s_dg[DG_T_FOLD], rtc()); }
         if (PCU && last) {
             // per-CU launch: this workgroup's counts per integral, once -- its per-CU word (a plain

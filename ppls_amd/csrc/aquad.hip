@@ -345,6 +345,104 @@ __global__ __launch_bounds__(FOLD_T) void k_level_fold(const LevelPart* __restri
     acc[5] = fmax(acc[5], s_v[0]);
 }
 
+// The frontier's narrow levels in ONE launch: a single workgroup runs `levels`
+// consecutive levels, level depth + k reading counts[depth + k] records from buf[k & 1] and writing
+// its children to buf[(k + 1) & 1] and their number to counts[depth + k + 1]. The appends need no
+// global atomic (one block: a block-wide prefix of the wave counts in LDS), the levels no host round
+// trip and no launch each (the tree's first ~13 levels hold <= 8 k records: launch- and
+// latency-bound as one launch per level, 2 launches each with the fold). The block's accumulators go
+// into d_acc once at the end, as k_level_fold's would.
+constexpr int NARROW_T = 1024;
+template <int FID>
+__global__ __launch_bounds__(NARROW_T) void k_level_narrow(Rec* __restrict__ buf0, Rec* __restrict__ buf1, unsigned cap,
+                                                           unsigned* __restrict__ counts, int d0, int levels, double eps,
+                                                           int max_depth, double* __restrict__ acc,
+                                                           const ExpPair* __restrict__ gtab) {
+    constexpr int NWV = NARROW_T / 64;
+    __shared__ ExpEntry tab[128];
+    __shared__ unsigned s_wc[NWV];
+    __shared__ unsigned s_n;
+    __shared__ double s_h[NWV], s_l[NWV];
+    __shared__ unsigned s_t[NWV], s_a[NWV], s_e[NWV], s_v[NWV];
+    stage_exp_table(tab, gtab);
+    if (threadIdx.x == 0) s_n = min(counts[d0], cap);
+    __syncthreads();
+    double hi = 0.0, lo = 0.0;
+    unsigned tasks = 0, leaves = 0, err = 0, lev = 0;
+    const unsigned w = threadIdx.x >> 6;
+    for (int k = 0; k < levels; ++k) {
+        const int depth = d0 + k;
+        const Rec* __restrict__ in = (k & 1) ? buf1 : buf0;
+        Rec* __restrict__ out = (k & 1) ? buf0 : buf1;
+        const unsigned n_in = s_n;
+        unsigned n_ref = 0;   // refining records of this level so far (block-uniform)
+        for (unsigned base = 0; base < n_in; base += NARROW_T) {
+            const unsigned i = base + threadIdx.x;
+            const bool active = i < n_in;
+            const Rec rc = active ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
+            double x[1] = {(rc.l + rc.r) / 2}, f[1];                       // :187
+            integrand_k<FID, 1>(x, f, tab);                                 // :188
+            const double lrarea = (rc.fl + rc.fr) * (rc.r - rc.l) / 2;      // :185
+            const double larea = (rc.fl + f[0]) * (x[0] - rc.l) / 2;        // :189
+            const double rarea = (f[0] + rc.fr) * (rc.r - x[0]) / 2;        // :190
+            bool refine = false;
+            if (active) {
+                ++tasks;
+                lev = max(lev, (unsigned)depth + 1u);
+                if (!(fabs((larea + rarea) - lrarea) > eps)) {              // :191
+                    dd_add(hi, lo, larea + rarea);                          // :199 -> :149
+                    ++leaves;
+                } else if (depth + 1 >= max_depth) {
+                    err |= ERRB_DEPTH;
+                } else {
+                    refine = true;
+                }
+            }
+            const unsigned long long m = __ballot(refine);
+            if (lane_id() == 0) s_wc[w] = (unsigned)__popcll(m);
+            __syncthreads();
+            unsigned off = n_ref, tot = 0;
+            for (unsigned v = 0; v < (unsigned)NWV; ++v) {
+                const unsigned c = s_wc[v];
+                off += v < w ? c : 0u;
+                tot += c;
+            }
+            __syncthreads();   // s_wc is rewritten by the next chunk
+            if (refine) {
+                const unsigned pos = 2u * (off + mbcnt(m));
+                if (pos + 1 < cap) {
+                    out[pos] = Rec{rc.l, x[0], rc.fl, f[0]};        // [l, mid]  (:192-194)
+                    out[pos + 1] = Rec{x[0], rc.r, f[0], rc.fr};    // [mid, r]  (:195-197)
+                } else {
+                    err |= ERRB_OVERFLOW;
+                }
+            }
+            n_ref += tot;
+        }
+        __syncthreads();   // the level's children are written (and visible to the block) before the next reads them
+        if (threadIdx.x == 0) {
+            counts[depth + 1] = 2u * n_ref;
+            s_n = min(2u * n_ref, cap);
+        }
+        __syncthreads();
+    }
+    wave_sum_dd(hi, lo);
+    const unsigned wt = wave_sum_u(tasks), wl = wave_sum_u(leaves), we = wave_or_u(err), wv = wave_max_u(lev);
+    if (lane_id() == 0) { s_h[w] = hi; s_l[w] = lo; s_t[w] = wt; s_a[w] = wl; s_e[w] = we; s_v[w] = wv; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double H = acc[0], L = acc[1];
+        unsigned T = 0, A = 0, E = 0, V = 0;
+        for (int v = 0; v < NWV; ++v) {
+            dd_add_dd(H, L, s_h[v], s_l[v]);
+            T += s_t[v]; A += s_a[v]; E |= s_e[v]; V = max(V, s_v[v]);
+        }
+        acc[0] = H; acc[1] = L; acc[2] += (double)T; acc[3] += (double)A;
+        acc[4] = (double)((unsigned)acc[4] | E);
+        acc[5] = fmax(acc[5], (double)V);
+    }
+}
+
 template <int FID>
 __global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* out, const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[128];

@@ -94,6 +94,14 @@ class HipStepper:
                                                 base + 4 * (depth + 1), acc.data_ptr()),
                "aq_level_step_chained")
 
+    def narrow(self, integrand, fronts, counts, depth, levels, cap, eps, max_depth, acc):
+        """`levels` levels from `depth` in ONE single-workgroup launch (aq_level_narrow): level depth + k
+        reads fronts[k % 2] and writes fronts[(k + 1) % 2]."""
+        base = counts.data_ptr()
+        _check(self.ctx.L.aq_level_narrow(self.ctx._h, integrand, fronts[0].data_ptr(), fronts[1].data_ptr(), int(cap),
+                                          base, int(depth), int(levels), float(eps), int(max_depth), acc.data_ptr()),
+               "aq_level_narrow")
+
     def sync(self):
         self.ctx.synchronize()
 
@@ -113,6 +121,11 @@ class FrontierResult:
 
 
 CHAIN_LEVELS = 4   # one GPU: levels chained on the device between host looks at the frontier size
+NARROW_LEVELS = 13  # the tree's first levels (<= 2^12 records each) in one single-workgroup launch
+
+
+def n_levels_narrow(max_depth: int) -> int:
+    return max(0, min(NARROW_LEVELS, max_depth - 1))
 
 
 def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebalance_every: int = 1,
@@ -159,6 +172,17 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     max_front = 1
     per_level = []
     bound = n   # chained: an upper bound of this rank's current frontier (children <= 2 x parents)
+    narrow = getattr(stepper, "narrow", None) if chain is not None else None
+    if narrow is not None and n_levels_narrow(max_depth) > 0:
+        # levels 0 .. NARROW_LEVELS-1 (at most 2^(NARROW_LEVELS-1) records each) in one launch
+        L0 = n_levels_narrow(max_depth)
+        try:
+            narrow(integrand, fronts, counts, 0, L0, capacity, problem.eps, max_depth, acc)
+        except AquadError as e:
+            raise AquadError(f"frontier: {e}")
+        depth = L0
+        cur = L0 % 2
+        bound = min(1 << L0, capacity)
     while True:
         nxt = 1 - cur
         # a local failure is carried through the size exchange as a negative count, so every rank

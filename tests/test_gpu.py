@@ -282,6 +282,29 @@ def test_sync_call_leaves_async_slots_alone(ctx, trees):
     assert (r.tasks, r.accepted) == (g3["tasks"], g3["leaves"])
 
 
+def test_cu_task_counters_every_launch(ctx, trees):
+    """per-CU task counters on every launch shape (the farmer's tasks_per_process,
+    aquadPartA.c:162). A pipelined bench-shape batch: the counters over all its launches sum to the
+    tasks of every integral, and every CU ran some; a lone integral: they equal its per-CU row."""
+    from ppls_amd import Problem
+    g8, g10 = trees["cosh4_eps1e-8"], trees["cosh4_eps1e-10"]
+    ctx.set_level_histograms(False)
+    try:
+        ctx.cu_task_counters(reset=True)
+        k = 4096
+        for _ in range(3):                     # three pipelined launches, no host sync between them
+            ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-8, first_slot=0)
+        cu = ctx.cu_task_counters(reset=True)
+        assert sum(cu.values()) == 3 * k * g8["tasks"]
+        assert len(cu) == ctx.num_cus
+        r = ctx.integrate(Problem(eps=1e-10))
+        cu1 = ctx.cu_task_counters(reset=True)
+        assert sum(cu1.values()) == r.tasks == g10["tasks"]
+        assert cu1 == r.tasks_per_cu
+    finally:
+        ctx.set_level_histograms(True)
+
+
 def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
     """MAXK integrals with random bounds in ONE persistent launch (the bench's launch shape); the
     first 256 against the committed golden fixture, all of them against the oracle."""
