@@ -198,6 +198,11 @@ int aq_level_step_chained(aq_ctx *ctx, int integrand, const double *d_in, const 
                           double *d_out, uint32_t cap_out, double eps, int depth, int max_depth, uint32_t *d_n_out,
                           double *d_acc);
 
+/* Deferred folds: while enabled, the level steps leave their per-block partial rows pending and ONE
+ * fold adds them into the accumulator later -- at aq_synchronize, at a step with another d_acc, or
+ * when disabling (the chained engine's levels between two host looks then cost one launch each, not
+ * two). d_acc is complete once aq_synchronize returns. */
+int aq_level_defer_fold(aq_ctx *ctx, int enable);
 /* `levels` consecutive levels in ONE single-workgroup launch (the narrow top of the tree, where a
  * launch per level is launch- and latency-bound): level depth + k reads d_counts[depth + k] records
  * from d_buf{k & 1} and appends its children to d_buf{(k + 1) & 1} (at most cap records), writing

@@ -204,12 +204,25 @@ struct LevelPart {
 #endif
 constexpr int LEVEL_R = AQ_LEVEL_R;
 
+// Child offsets by a decoupled look-back scan over the chunks (r03): chunk c publishes its refining
+// count (AGG) in status[c], adds up its predecessors' published values back to the first inclusive
+// prefix (PRE), and publishes its own prefix. No atomic on one counter -- r02's one atomicAdd per
+// chunk was a serial fan-in at the wide levels (1.6 k atomics on one line per level) -- and the
+// children land in chunk order, the same layout on every run. A status word: epoch (bits 40-63, one
+// per level launch, so the array is never reset) | PRE flag (bit 39) | count (bits 0-31).
+constexpr unsigned long long LB_PRE = 1ull << 39;
+constexpr int LB_MAX_CHUNKS = 1 << 16;   // status words per context (>= frontier capacity / chunk)
+__device__ __forceinline__ unsigned long long lb_word(unsigned epoch, bool pre, unsigned count) {
+    return ((unsigned long long)epoch << 40) | (pre ? LB_PRE : 0ull) | (unsigned long long)count;
+}
+
 template <int FID>
 __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
                                                     unsigned* __restrict__ n_out, unsigned cap_out, double eps,
                                                     int depth, int max_depth, LevelPart* __restrict__ parts,
                                                     const ExpPair* __restrict__ gtab,
-                                                    const unsigned* __restrict__ n_in_dev) {
+                                                    const unsigned* __restrict__ n_in_dev,
+                                                    unsigned long long* __restrict__ status, unsigned epoch) {
     constexpr int R = LEVEL_R;
     // chained levels: the count a previous step appended (read once; uniform), clamped to n_in = the
     // host's bound (<= the input buffer's capacity; a count beyond it was flagged as an overflow)
@@ -264,12 +277,31 @@ __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, 
             m[k] = __ballot(refine[k]);
             c[k + 1] = c[k] + (unsigned)__popcll(m[k]);
         }
-        // one atomic for the block's chunk
+        // the chunk's offset: decoupled look-back over the preceding chunks (see lb_word)
         if (lane_id() == 0) s_wc[parity][w] = c[R];
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned tot = s_wc[parity][0] + s_wc[parity][1] + s_wc[parity][2] + s_wc[parity][3];
-            s_base[parity] = tot ? atomicAdd(n_out, 2u * tot) : 0u;
+            const unsigned ci = base / chunk;
+            unsigned excl = 0;
+            if (ci == 0) {
+                st_wt64(&status[0], lb_word(epoch, true, tot));
+            } else {
+                st_wt64(&status[ci], lb_word(epoch, false, tot));
+                for (unsigned j = ci - 1;;) {
+                    const unsigned long long v = ld_wt64(&status[j]);
+                    if ((unsigned)(v >> 40) != (epoch & 0xffffffu)) {   // not published yet
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    excl += (unsigned)v;
+                    if ((v & LB_PRE) || j == 0) break;
+                    --j;
+                }
+                st_wt64(&status[ci], lb_word(epoch, true, excl + tot));
+            }
+            s_base[parity] = 2u * excl;
+            if (base + chunk >= n_in) *n_out = 2u * (excl + tot);   // the last chunk: the level's children
         }
         __syncthreads();
         unsigned off = s_base[parity];
