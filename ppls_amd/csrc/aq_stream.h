@@ -732,6 +732,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             bot -= pf_n;
             if (lane < pf_n) lds_store6(ring_addr(ring8, ring_slot(bot) + lane, ring_vmask), pf);
+            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }   // landed
             __builtin_amdgcn_wave_barrier();   // reconverge here: the ring indices stay wave-uniform
             pf_n = 0;
         }
@@ -1323,7 +1324,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // (same-wave, same-address order: no wait for the spills)
             pf = chunk_load(&cel->c[ctop / 64u], lane);
             __builtin_amdgcn_wave_barrier();
-            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)pf_n); }
         }
 
         // ---- a burst of rounds: the hot loop. It runs while the ring neither empties nor nears
@@ -1473,13 +1473,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     b_bot -= b_pf;
                     if (lane < b_pf) lds_store6(ring_addr(ring8, ring_slot(b_bot) + lane, ring_vmask), pf);
+                    if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)b_pf); }
                     b_pf = 0;
                     b_go = true;
                 } else if ((AQ_INB_MASK & 4) && PREFETCH && b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
                     b_pf = 64u;
                     b_ctop -= 64u;
                     pf = chunk_load(&cel->c[b_ctop / 64u], lane);
-                    if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], 64ull); }
                     b_go = true;
                 }
                 if (b_go) {

@@ -203,40 +203,37 @@ struct LevelPart {
 #define AQ_LEVEL_R 4
 #endif
 constexpr int LEVEL_R = AQ_LEVEL_R;
-
-// Child offsets by a decoupled look-back scan over the chunks (r03): chunk c publishes its refining
-// count (AGG) in status[c], adds up its predecessors' published values back to the first inclusive
-// prefix (PRE), and publishes its own prefix. No atomic on one counter -- r02's one atomicAdd per
-// chunk was a serial fan-in at the wide levels (1.6 k atomics on one line per level) -- and the
-// children land in chunk order, the same layout on every run. A status word: epoch (bits 40-63, one
-// per level launch, so the array is never reset) | PRE flag (bit 39) | count (bits 0-31).
-constexpr unsigned long long LB_PRE = 1ull << 39;
-constexpr int LB_MAX_CHUNKS = 1 << 16;   // status words per context (>= frontier capacity / chunk)
-__device__ __forceinline__ unsigned long long lb_word(unsigned epoch, bool pre, unsigned count) {
-    return ((unsigned long long)epoch << 40) | (pre ? LB_PRE : 0ull) | (unsigned long long)count;
-}
+// Threads per block (a chunk of LEVEL_T x LEVEL_R records per append). r03 A/B over cosh4 eps=1e-12
+// under rocprofv3 (tools/frontier_ab.sh; profiles/r03_ab/frontier_ab.txt): widest level 256 threads
+// 33.5 us, 512 33.2, 1024 37.6, 1024 x 8 records 54.4; a decoupled look-back scan in place of the
+// atomic (chunk-ordered output, wave-parallel look-back) 40.4 us -- the PRE frontier advances ~64
+// chunks per L2 round trip while all 1.6 k chunks finish at once, slower than the atomics' fan-in.
+#ifndef AQ_LEVEL_T
+#define AQ_LEVEL_T 256
+#endif
+constexpr int LEVEL_T = AQ_LEVEL_T;
+constexpr int LEVEL_NW = LEVEL_T / 64;
 
 template <int FID>
-__global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
+__global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
                                                     unsigned* __restrict__ n_out, unsigned cap_out, double eps,
                                                     int depth, int max_depth, LevelPart* __restrict__ parts,
                                                     const ExpPair* __restrict__ gtab,
-                                                    const unsigned* __restrict__ n_in_dev,
-                                                    unsigned long long* __restrict__ status, unsigned epoch) {
+                                                    const unsigned* __restrict__ n_in_dev) {
     constexpr int R = LEVEL_R;
     // chained levels: the count a previous step appended (read once; uniform), clamped to n_in = the
     // host's bound (<= the input buffer's capacity; a count beyond it was flagged as an overflow)
     if (n_in_dev) n_in = min(*n_in_dev, n_in);
     __shared__ ExpEntry tab[128];
-    __shared__ double s_h[4], s_l[4];
-    __shared__ unsigned s_t[4], s_a[4], s_e[4];
-    __shared__ unsigned s_wc[2][4], s_base[2];
+    __shared__ double s_h[LEVEL_NW], s_l[LEVEL_NW];
+    __shared__ unsigned s_t[LEVEL_NW], s_a[LEVEL_NW], s_e[LEVEL_NW];
+    __shared__ unsigned s_wc[2][LEVEL_NW], s_base[2];
     stage_exp_table(tab, gtab);
     __syncthreads();
     double hi = 0.0, lo = 0.0;
     unsigned tasks = 0, leaves = 0, err = 0;
     const unsigned w = threadIdx.x >> 6;
-    const unsigned chunk = 256u * R;
+    const unsigned chunk = (unsigned)LEVEL_T * R;
     unsigned parity = 0;
     // the loop bound depends on blockIdx only: every thread of the block runs every chunk (barriers)
     for (unsigned base = blockIdx.x * chunk; base < n_in; base += gridDim.x * chunk, parity ^= 1u) {
@@ -245,7 +242,7 @@ __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, 
         double x[R], f[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-            const unsigned i = base + (unsigned)k * 256u + threadIdx.x;
+            const unsigned i = base + (unsigned)k * (unsigned)LEVEL_T + threadIdx.x;
             active[k] = i < n_in;
             rc[k] = active[k] ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
             x[k] = (rc[k].l + rc[k].r) / 2;                              // :187
@@ -277,31 +274,13 @@ __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, 
             m[k] = __ballot(refine[k]);
             c[k + 1] = c[k] + (unsigned)__popcll(m[k]);
         }
-        // the chunk's offset: decoupled look-back over the preceding chunks (see lb_word)
+        // the chunk's offset: one atomic per block and chunk
         if (lane_id() == 0) s_wc[parity][w] = c[R];
         __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned tot = s_wc[parity][0] + s_wc[parity][1] + s_wc[parity][2] + s_wc[parity][3];
-            const unsigned ci = base / chunk;
-            unsigned excl = 0;
-            if (ci == 0) {
-                st_wt64(&status[0], lb_word(epoch, true, tot));
-            } else {
-                st_wt64(&status[ci], lb_word(epoch, false, tot));
-                for (unsigned j = ci - 1;;) {
-                    const unsigned long long v = ld_wt64(&status[j]);
-                    if ((unsigned)(v >> 40) != (epoch & 0xffffffu)) {   // not published yet
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    excl += (unsigned)v;
-                    if ((v & LB_PRE) || j == 0) break;
-                    --j;
-                }
-                st_wt64(&status[ci], lb_word(epoch, true, excl + tot));
-            }
-            s_base[parity] = 2u * excl;
-            if (base + chunk >= n_in) *n_out = 2u * (excl + tot);   // the last chunk: the level's children
+        if (threadIdx.x == 0) {   // one atomic for the block's chunk
+            unsigned tot = 0;
+            for (int v = 0; v < LEVEL_NW; ++v) tot += s_wc[parity][v];
+            s_base[parity] = tot ? atomicAdd(n_out, 2u * tot) : 0u;
         }
         __syncthreads();
         unsigned off = s_base[parity];
@@ -326,7 +305,7 @@ __global__ __launch_bounds__(256) void k_level_step(const Rec* __restrict__ in, 
     if (threadIdx.x == 0) {
         double H = 0.0, L = 0.0;
         unsigned T = 0, A = 0, E = 0;
-        for (int k = 0; k < 4; ++k) { dd_add_dd(H, L, s_h[k], s_l[k]); T += s_t[k]; A += s_a[k]; E |= s_e[k]; }
+        for (int k = 0; k < LEVEL_NW; ++k) { dd_add_dd(H, L, s_h[k], s_l[k]); T += s_t[k]; A += s_a[k]; E |= s_e[k]; }
         LevelPart p;
         p.hi = H; p.lo = L; p.tasks = (double)T; p.leaves = (double)A; p.err = (double)E;
         p.levels = T ? (double)(depth + 1) : 0.0;

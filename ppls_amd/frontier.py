@@ -180,136 +180,137 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     if defer is not None:
         defer(True)   # one fold per host look instead of one per level (aq_level_defer_fold)
     try:
-            narrow = getattr(stepper, "narrow", None) if chain is not None else None
-            if narrow is not None and n_levels_narrow(max_depth) > 0:
-                # levels 0 .. NARROW_LEVELS-1 (at most 2^(NARROW_LEVELS-1) records each) in one launch
-                L0 = n_levels_narrow(max_depth)
+        # one GPU: the narrow top in one launch (several ranks keep their per-level rebalancing from level 0)
+        narrow = getattr(stepper, "narrow", None) if (chain is not None and world == 1) else None
+        if narrow is not None and n_levels_narrow(max_depth) > 0:
+            # levels 0 .. NARROW_LEVELS-1 (at most 2^(NARROW_LEVELS-1) records each) in one launch
+            L0 = n_levels_narrow(max_depth)
+            try:
+                narrow(integrand, fronts, counts, 0, L0, capacity, problem.eps, max_depth, acc)
+            except AquadError as e:
+                raise AquadError(f"frontier: {e}")
+            depth = L0
+            cur = L0 % 2
+            bound = min(1 << L0, capacity)
+        while True:
+            nxt = 1 - cur
+            # a local failure is carried through the size exchange as a negative count, so every rank
+            # raises together instead of the others waiting in the collective (one all-gather per level)
+            err = ""
+            synced = True
+            if depth >= max_depth + 1:
+                err = "maximum refinement depth reached"
+                produced = 0
+            elif chain is not None:
                 try:
-                    narrow(integrand, fronts, counts, 0, L0, capacity, problem.eps, max_depth, acc)
+                    chain(integrand, fronts[cur], counts, depth, bound, fronts[nxt], capacity, problem.eps, max_depth, acc)
                 except AquadError as e:
-                    raise AquadError(f"frontier: {e}")
-                depth = L0
-                cur = L0 % 2
-                bound = min(1 << L0, capacity)
-            while True:
-                nxt = 1 - cur
-                # a local failure is carried through the size exchange as a negative count, so every rank
-                # raises together instead of the others waiting in the collective (one all-gather per level)
-                err = ""
-                synced = True
-                if depth >= max_depth + 1:
-                    err = "maximum refinement depth reached"
-                    produced = 0
-                elif chain is not None:
-                    try:
-                        chain(integrand, fronts[cur], counts, depth, bound, fronts[nxt], capacity, problem.eps, max_depth, acc)
-                    except AquadError as e:
-                        err = str(e)
-                    bound = min(2 * bound, capacity)
-                    synced = bool(err) or (depth + 1) % sync_every == 0
-                    produced = 0
-                    if synced and not err:
-                        stepper.sync()
-                        produced = int(counts[depth + 1].item())
-                        if produced > capacity:
-                            err = f"capacity exceeded: {produced} > {capacity}"
-                else:
-                    try:
-                        stepper.step(integrand, fronts[cur], n, fronts[nxt], capacity, problem.eps, depth, max_depth, nout,
-                                     acc)
-                        stepper.sync()
-                        produced = int(nout.item())
-                    except AquadError as e:
-                        err, produced = str(e), 0
-                    if not err and produced > capacity:
+                    err = str(e)
+                bound = min(2 * bound, capacity)
+                synced = bool(err) or (depth + 1) % sync_every == 0
+                produced = 0
+                if synced and not err:
+                    stepper.sync()
+                    produced = int(counts[depth + 1].item())
+                    if produced > capacity:
                         err = f"capacity exceeded: {produced} > {capacity}"
-                    per_level.append(n)
-                cur, depth = nxt, depth + 1
-                if not synced:
-                    continue
-                n = 0 if err else produced
-                bound = n
-                mysize = torch.tensor([-1 if err else n], dtype=torch.int64, device=comm_dev)
-                if distributed:
-                    gathered = [torch.zeros(1, dtype=torch.int64, device=comm_dev) for _ in range(world)]
-                    dist.all_gather(gathered, mysize, group=group)
-                    sizes = [int(g.item()) for g in gathered]
-                else:
-                    sizes = [-1 if err else n]
-                failed = [r for r, v in enumerate(sizes) if v < 0]
-                if failed:
-                    raise AquadError(f"frontier: rank {failed[0]} failed" + (f" ({err})" if err else ""))
-                total = sum(sizes)
-                max_front = max(max_front, total)
-                if total == 0:
-                    break
-                if world > 1 and depth % rebalance_every == 0:
-                    moves = plan_moves(sizes)
-                    if moves:
-                        rebalances += 1
-                        ops = []
-                        staged = []        # (device slice, host buffer): a CPU backend (gloo) with device records
-                        send_end = n
-                        recv_at = n
-                        for src, dst, k in moves:
-                            moved += k
-                            if src == rank:
-                                buf = fronts[cur][send_end - k:send_end]
-                                if buf.device != comm_dev:
-                                    buf = buf.to(comm_dev)
-                                ops.append(dist.P2POp(dist.isend, buf, dst, group))
-                                send_end -= k
-                            elif dst == rank:
-                                if recv_at + k > capacity:   # every rank computes the same plan: all raise together
-                                    raise AquadError(f"frontier capacity exceeded on rank {rank} while receiving")
-                                buf = fronts[cur][recv_at:recv_at + k]
-                                if buf.device != comm_dev:
-                                    host = torch.empty((k, REC), dtype=torch.float64, device=comm_dev)
-                                    staged.append((buf, host))
-                                    buf = host
-                                ops.append(dist.P2POp(dist.irecv, buf, src, group))
-                                recv_at += k
-                        if ops:
-                            for req in dist.batch_isend_irecv(ops):
-                                req.wait()
-                        for dst_slice, host in staged:
-                            dst_slice.copy_(host)
-                        n = send_end + (recv_at - n)      # a rank only sends or only receives
-                        bound = n
-                        if counts is not None:
-                            counts[depth] = n             # the next chained step reads it on the device
-                        if dev.type == "cuda":
-                            torch.cuda.synchronize(dev)   # the next level runs on the engine's own stream
-            stepper.sync()
-            if counts is not None:
-                per_level = [int(v) for v in counts[:depth].cpu()]
-            mine = acc.to(comm_dev)
-            if distributed:
-                accs = [torch.zeros(8, dtype=torch.float64, device=comm_dev) for _ in range(world)]
-                dist.all_gather(accs, mine, group=group)
-                lv = torch.tensor(per_level, dtype=torch.int64, device=comm_dev)
-                # per-level task counts: ranks ran the same number of levels (one collective per level)
-                dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
-                per_level = [int(v) for v in lv.cpu()]
             else:
-                accs = [mine]
-            while per_level and per_level[-1] == 0:   # chained levels past the last sync point
-                per_level.pop()
-            rows = [a.cpu().numpy() for a in accs]
-            hi = lo = 0.0
-            for r in rows:
-                hi, lo = dd_add(hi, lo, float(r[0]), float(r[1]))
-            err = 0
-            for r in rows:
-                err |= int(r[4])
-            if err:
-                msg = "; ".join(v for k, v in ERR_NAMES.items() if err & k)
-                raise AquadError(f"frontier: {msg}")
-            tasks = [int(r[2]) for r in rows]
-            leaves = [int(r[3]) for r in rows]
-            return FrontierResult(area=hi + lo, tasks=sum(tasks), accepted=sum(leaves), levels=int(max(r[5] for r in rows)),
-                                  tasks_per_rank=tasks, accepted_per_rank=leaves, tasks_per_level=per_level,
-                                  rebalances=rebalances, moved_records=moved, max_frontier=max_front)
+                try:
+                    stepper.step(integrand, fronts[cur], n, fronts[nxt], capacity, problem.eps, depth, max_depth, nout,
+                                 acc)
+                    stepper.sync()
+                    produced = int(nout.item())
+                except AquadError as e:
+                    err, produced = str(e), 0
+                if not err and produced > capacity:
+                    err = f"capacity exceeded: {produced} > {capacity}"
+                per_level.append(n)
+            cur, depth = nxt, depth + 1
+            if not synced:
+                continue
+            n = 0 if err else produced
+            bound = n
+            mysize = torch.tensor([-1 if err else n], dtype=torch.int64, device=comm_dev)
+            if distributed:
+                gathered = [torch.zeros(1, dtype=torch.int64, device=comm_dev) for _ in range(world)]
+                dist.all_gather(gathered, mysize, group=group)
+                sizes = [int(g.item()) for g in gathered]
+            else:
+                sizes = [-1 if err else n]
+            failed = [r for r, v in enumerate(sizes) if v < 0]
+            if failed:
+                raise AquadError(f"frontier: rank {failed[0]} failed" + (f" ({err})" if err else ""))
+            total = sum(sizes)
+            max_front = max(max_front, total)
+            if total == 0:
+                break
+            if world > 1 and depth % rebalance_every == 0:
+                moves = plan_moves(sizes)
+                if moves:
+                    rebalances += 1
+                    ops = []
+                    staged = []        # (device slice, host buffer): a CPU backend (gloo) with device records
+                    send_end = n
+                    recv_at = n
+                    for src, dst, k in moves:
+                        moved += k
+                        if src == rank:
+                            buf = fronts[cur][send_end - k:send_end]
+                            if buf.device != comm_dev:
+                                buf = buf.to(comm_dev)
+                            ops.append(dist.P2POp(dist.isend, buf, dst, group))
+                            send_end -= k
+                        elif dst == rank:
+                            if recv_at + k > capacity:   # every rank computes the same plan: all raise together
+                                raise AquadError(f"frontier capacity exceeded on rank {rank} while receiving")
+                            buf = fronts[cur][recv_at:recv_at + k]
+                            if buf.device != comm_dev:
+                                host = torch.empty((k, REC), dtype=torch.float64, device=comm_dev)
+                                staged.append((buf, host))
+                                buf = host
+                            ops.append(dist.P2POp(dist.irecv, buf, src, group))
+                            recv_at += k
+                    if ops:
+                        for req in dist.batch_isend_irecv(ops):
+                            req.wait()
+                    for dst_slice, host in staged:
+                        dst_slice.copy_(host)
+                    n = send_end + (recv_at - n)      # a rank only sends or only receives
+                    bound = n
+                    if counts is not None:
+                        counts[depth] = n             # the next chained step reads it on the device
+                    if dev.type == "cuda":
+                        torch.cuda.synchronize(dev)   # the next level runs on the engine's own stream
+        stepper.sync()
+        if counts is not None:
+            per_level = [int(v) for v in counts[:depth].cpu()]
+        mine = acc.to(comm_dev)
+        if distributed:
+            accs = [torch.zeros(8, dtype=torch.float64, device=comm_dev) for _ in range(world)]
+            dist.all_gather(accs, mine, group=group)
+            lv = torch.tensor(per_level, dtype=torch.int64, device=comm_dev)
+            # per-level task counts: ranks ran the same number of levels (one collective per level)
+            dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+            per_level = [int(v) for v in lv.cpu()]
+        else:
+            accs = [mine]
+        while per_level and per_level[-1] == 0:   # chained levels past the last sync point
+            per_level.pop()
+        rows = [a.cpu().numpy() for a in accs]
+        hi = lo = 0.0
+        for r in rows:
+            hi, lo = dd_add(hi, lo, float(r[0]), float(r[1]))
+        err = 0
+        for r in rows:
+            err |= int(r[4])
+        if err:
+            msg = "; ".join(v for k, v in ERR_NAMES.items() if err & k)
+            raise AquadError(f"frontier: {msg}")
+        tasks = [int(r[2]) for r in rows]
+        leaves = [int(r[3]) for r in rows]
+        return FrontierResult(area=hi + lo, tasks=sum(tasks), accepted=sum(leaves), levels=int(max(r[5] for r in rows)),
+                              tasks_per_rank=tasks, accepted_per_rank=leaves, tasks_per_level=per_level,
+                              rebalances=rebalances, moved_records=moved, max_frontier=max_front)
     finally:
         if defer is not None:
             defer(False)

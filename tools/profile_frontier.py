@@ -17,6 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "k_level_step"
+NARROW = 13   # ppls_amd/frontier.py NARROW_LEVELS
 REC = 32
 FLOP = 38
 FP64_PEAK = 78.6e12
@@ -55,7 +56,20 @@ def main():
     nlev = len(tpl)
     tr = [r for r in rows(os.path.join(d, "kt", "**", "*kernel_trace.csv"))]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    runs = [r for r in split_runs([r for r in tr if KERNEL in r["Kernel_Name"]], "Grid_Size_X") if len(r) >= nlev]
+    # r03: one GPU runs the first NARROW levels in one k_level_narrow dispatch; the k_level_step
+    # dispatches of a call then start at level NARROW (a call = the dispatches after a narrow one)
+    narrows = [r for r in tr if "k_level_narrow" in r["Kernel_Name"]]
+    first = 0
+    if narrows:
+        first = NARROW
+        starts = [int(r["Start_Timestamp"]) for r in narrows] + [1 << 62]
+        steps = [r for r in tr if KERNEL in r["Kernel_Name"]]
+        runs = [[r for r in steps if starts[i] < int(r["Start_Timestamp"]) < starts[i + 1]] for i in range(len(narrows))]
+        runs = [r for r in runs if len(r) >= nlev - first]
+        narrow_us = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in narrows)
+    else:
+        runs = [r for r in split_runs([r for r in tr if KERNEL in r["Kernel_Name"]], "Grid_Size_X") if len(r) >= nlev]
+        narrow_us = []
     if not runs:
         sys.exit("no complete run of %d level dispatches" % nlev)
     timed = runs[1:] or runs   # the first call is the warmup
@@ -63,16 +77,27 @@ def main():
     fold_us = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in folds)
 
     def pmc(name):
-        rs = [r for r in rows(os.path.join(d, name.lower(), "**", "*counter_collection.csv"))
-              if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == name]
-        rs.sort(key=lambda r: int(r["Dispatch_Id"]))
+        allr = [r for r in rows(os.path.join(d, name.lower(), "**", "*counter_collection.csv")) if r["Counter_Name"] == name]
+        allr.sort(key=lambda r: int(r["Dispatch_Id"]))
+        if narrows:
+            rr, cur = [], None
+            for r in allr:
+                if "k_level_narrow" in r["Kernel_Name"]:
+                    cur = []
+                    rr.append(cur)
+                elif KERNEL in r["Kernel_Name"] and cur is not None:
+                    cur.append(r)
+            rr = [x for x in rr if len(x) >= nlev - first]
+            return [[float(x["Counter_Value"]) for x in run[:nlev - first]] for run in rr] or None
+        rs = [r for r in allr if KERNEL in r["Kernel_Name"]]
         rr = [x for x in split_runs(rs, "Grid_Size") if len(x) >= nlev]
         return [[float(x["Counter_Value"]) for x in run[:nlev]] for run in rr] or None
 
     fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
     levels = []
-    for lev in range(nlev):
-        durs = sorted((int(run[lev]["End_Timestamp"]) - int(run[lev]["Start_Timestamp"])) * 1e-9 for run in timed)
+    for lev in range(first, nlev):
+        i = lev - first
+        durs = sorted((int(run[i]["End_Timestamp"]) - int(run[i]["Start_Timestamp"])) * 1e-9 for run in timed)
         t = durs[len(durs) // 2]
         n_in, n_out = tpl[lev], 2 * (tpl[lev] - lpl[lev])
         alg = REC * (n_in + n_out)
@@ -80,7 +105,7 @@ def main():
              "alg_bytes": alg, "alg_GBps": round(alg / t / 1e9, 1), "hbm_frac_alg": round(alg / t / HBM_PEAK, 4),
              "fp64_frac": round(FLOP * n_in / t / FP64_PEAK, 4)}
         if fetch and write:
-            hb = sorted((2 * f[lev] + w[lev]) * 1024 for f, w in zip(fetch, write))
+            hb = sorted((2 * f[i] + w[i]) * 1024 for f, w in zip(fetch, write))
             e["hbm_bytes_measured"] = hb[len(hb) // 2]
         levels.append(e)
     tot_t = sum(e["us"] for e in levels) * 1e-6
@@ -88,6 +113,7 @@ def main():
     widest = max(levels, key=lambda e: e["records_in"])
     print(json.dumps({"kernel": KERNEL, "workload": key, "levels": nlev, "runs_timed": len(timed),
                       "dispatches_per_run": [len(r) for r in runs],
+                      "narrow_levels": first, "narrow_us_median": narrow_us[len(narrow_us) // 2] if narrow_us else None,
                       "sum_level_us": round(tot_t * 1e6, 1), "alg_bytes_total": tot_b,
                       "alg_GBps_overall": round(tot_b / tot_t / 1e9, 1),
                       "fp64_frac_overall": round(FLOP * sum(tpl) / tot_t / FP64_PEAK, 4),
