@@ -211,6 +211,13 @@ int aq_level_defer_fold(aq_ctx *ctx, int enable);
 int aq_level_narrow(aq_ctx *ctx, int integrand, double *d_buf0, double *d_buf1, uint32_t cap, uint32_t *d_counts,
                     int depth, int levels, double eps, int max_depth, double *d_acc);
 
+/* The frontier engine on ONE GPU with its host loop in C (ppls_amd/frontier.py's single-rank path):
+ * the root, the narrow top (aq_level_narrow), then chained level steps with deferred folds, the
+ * frontier size read every sync_every levels. Frontier buffers of cap records each are context-owned
+ * (grown on demand). Fills res and the per-level histograms (arrays of maxlev, or NULL). */
+int aq_frontier_integrate(aq_ctx *ctx, const aq_problem *p, uint32_t cap, int sync_every, aq_result *res,
+                          uint64_t *tasks_per_level, uint64_t *leaves_per_level, int maxlev);
+
 /* Per-level task / accepted histograms of the last aq_integrate* call (levels 0..maxlev-1). */
 int aq_level_histogram(aq_ctx *ctx, uint64_t *tasks_per_level, uint64_t *leaves_per_level, int maxlev);
 

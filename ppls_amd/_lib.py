@@ -17,7 +17,7 @@ EXPORTS = (
     "aq_exact_round", "aq_max_integrals_per_launch", "aq_integrate_many_async", "aq_integrate_mixed_async",
     "aq_synchronize", "aq_gather_results", "aq_gather_exact", "aq_integrate_levels", "aq_level_histogram",
     "aq_tasks_per_cu", "aq_cu_task_counters", "aq_integrate_batch", "aq_eval_integrand", "aq_eval_cosh", "aq_kernel_timing",
-    "aq_kernel_time", "aq_set_diagnostics", "aq_diagnostics", "aq_frontier_root", "aq_level_step", "aq_level_step_chained", "aq_level_narrow", "aq_level_defer_fold",
+    "aq_kernel_time", "aq_set_diagnostics", "aq_diagnostics", "aq_frontier_root", "aq_level_step", "aq_level_step_chained", "aq_level_narrow", "aq_level_defer_fold", "aq_frontier_integrate",
     "aq_group_create", "aq_group_unique_id", "aq_group_join", "aq_group_destroy", "aq_group_size",
     "aq_integrate_group", "aq_print_reference", "aq_print_reference_procs",
 )
@@ -91,6 +91,7 @@ def load(build_if_missing=True):
         "aq_level_histogram": ([vp, up, up, c_int], c_int),
         "aq_cu_task_counters": ([vp, up, c_int, c_int], c_int),
         "aq_level_defer_fold": ([vp, c_int], c_int),
+        "aq_frontier_integrate": ([vp, P, ctypes.c_uint32, c_int, R, up, up, c_int], c_int),
         "aq_level_narrow": ([vp, c_int, vp, vp, ctypes.c_uint32, vp, c_int, c_int, c_dbl, c_int, vp], c_int),
         "aq_tasks_per_cu": ([vp, up, c_int], c_int),
         "aq_integrate_batch": ([vp, ctypes.c_size_t, dp, dp, c_dbl, c_int, dp, up, up], c_int),

@@ -22,6 +22,7 @@ on the device; the final combine is one all-gather of them, folded on the host i
 Backends: the product stepper is HipStepper (the C ABI). Tests pass the oracle's CPU restatement
 (oracle/pyoracle.py: level_step) with the gloo backend to cover the multi-rank protocol on CPU.
 """
+import ctypes
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
@@ -102,6 +103,20 @@ class HipStepper:
                                           base, int(depth), int(levels), float(eps), int(max_depth), acc.data_ptr()),
                "aq_level_narrow")
 
+    def integrate_one_gpu(self, problem, capacity, sync_every=4):
+        """The whole single-GPU frontier run with its host loop in C (aq_frontier_integrate)."""
+        from .aquad import _up
+        r = _lib.aq_result()
+        t = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+        lv = np.zeros(_lib.AQ_MAX_LEVELS, np.uint64)
+        _check(self.ctx.L.aq_frontier_integrate(self.ctx._h, ctypes.byref(problem.c()), int(capacity), int(sync_every),
+                                                ctypes.byref(r), _up(t), _up(lv), _lib.AQ_MAX_LEVELS),
+               "aq_frontier_integrate")
+        per = [int(v) for v in t[:int(r.levels)]]
+        return FrontierResult(area=r.area, tasks=int(r.tasks), accepted=int(r.accepted), levels=int(r.levels),
+                              tasks_per_rank=[int(r.tasks)], accepted_per_rank=[int(r.accepted)], tasks_per_level=per,
+                              rebalances=0, moved_records=0, max_frontier=max(per) if per else 0)
+
     def defer_folds(self, enable: bool):
         """Level steps leave their partial rows for one fold at the next sync (aq_level_defer_fold)."""
         _check(self.ctx.L.aq_level_defer_fold(self.ctx._h, 1 if enable else 0), "aq_level_defer_fold")
@@ -133,7 +148,7 @@ def n_levels_narrow(max_depth: int) -> int:
 
 
 def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebalance_every: int = 1,
-              capacity: int = 1 << 22) -> FrontierResult:
+              capacity: int = 1 << 22, c_loop: bool = True) -> FrontierResult:
     """One integral over every rank of `group` (torch.distributed, initialised by the caller; a
     single process runs without one). Collective: every rank calls it with the same arguments.
 
@@ -141,7 +156,8 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     levels between sync points -- every `rebalance_every` levels with several ranks (where the sizes
     are exchanged and records moved), every CHAIN_LEVELS levels on one -- so the host reads the
     frontier size once per sync point instead of once per level. Steppers without it (the CPU
-    restatement in the tests) sync every level."""
+    restatement in the tests) sync every level. With one GPU and c_loop (the default) the same levels
+    run with their host loop in C (aq_frontier_integrate); c_loop=False keeps the Python loop."""
     problem = problem or Problem()
     if stepper is None:
         raise AquadError("frontier.integrate needs a stepper (HipStepper(ctx) on the GPU)")
@@ -156,6 +172,13 @@ def integrate(problem: Optional[Problem] = None, stepper=None, group=None, rebal
     comm_dev = dev if (distributed and dist.get_backend(group) == "nccl") else torch.device("cpu")
 
     chain = getattr(stepper, "chain_step", None) if dev.type == "cuda" else None
+    one_gpu = getattr(stepper, "integrate_one_gpu", None) if (c_loop and chain is not None and world == 1) else None
+    if one_gpu is not None:
+        # one GPU: no exchange to make -- the same levels with the host loop in C (aq_frontier_integrate)
+        try:
+            return one_gpu(problem, capacity, CHAIN_LEVELS)
+        except AquadError as e:
+            raise AquadError(f"frontier: {e}")
     sync_every = rebalance_every if world > 1 else CHAIN_LEVELS
     fronts = [torch.empty((capacity, REC), dtype=torch.float64, device=dev) for _ in range(2)]
     nout = torch.zeros(1, dtype=torch.int32, device=dev)

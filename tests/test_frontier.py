@@ -122,6 +122,24 @@ def test_frontier_hip_single_rank(trees):
 
 
 @pytest.mark.gpu
+def test_frontier_c_loop_equals_python_loop(trees):
+    """One GPU: the C host loop (aq_frontier_integrate) and the Python chained loop run the same levels:
+    identical counts and per-level histograms, areas within the double-double fold's rounding."""
+    from ppls_amd import Context, Problem, frontier
+    with Context(0) as ctx:
+        st = frontier.HipStepper(ctx)
+        for name in ("cosh4_eps1e-10", "sin_recip_eps1e-9"):
+            g = trees[name]
+            p = Problem(0 if g["integrand"] == "cosh4" else 1, g["a"], g["b"], g["eps"])
+            rc = frontier.integrate(p, stepper=st)
+            rp = frontier.integrate(p, stepper=st, c_loop=False)
+            assert (rc.tasks, rc.accepted, rc.levels) == (rp.tasks, rp.accepted, rp.levels) == (g["tasks"], g["leaves"],
+                                                                                                  g["levels"]), name
+            assert rc.tasks_per_level == rp.tasks_per_level == g["tasks_per_level"]
+            assert abs(rc.area - rp.area) <= 1e-13 * abs(rp.area)
+
+
+@pytest.mark.gpu
 def test_frontier_hip_capacity_overflow_raises():
     """A frontier wider than the buffers fails loudly on the chained path too (the device count
     passes the capacity between host looks; the kernel flags the dropped children)."""
