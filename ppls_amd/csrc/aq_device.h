@@ -195,6 +195,44 @@ __device__ __forceinline__ void pair_step_halves(double ha, double hb, double fa
     }
 }
 
+// pair_step_halves with the parent's doubled areas carried in (doubled-area integrands only). A child's
+// lrarea (:185) is token for token its parent's larea / rarea (:189 / :190: the same F values and
+// the same width m - a, b - m), so a pair that carries its parent's two products, lr0 = 2 larea and
+// lr1 = 2 rarea of the task it came from, needs no (fl + fr) * (r - l) of its own: six FP64 fewer per
+// pair. The children's values are each task's own l2 / r2, returned for the push.
+struct Step2c {
+    double fmid, l2, r2, area2;
+    bool refine;
+};
+template <int FID>
+__device__ __forceinline__ void pair_step_carry(double ha, double hb, double fa, double fm, double fb, double lr0,
+                                                double lr1, double eps2, const ExpEntry* __restrict__ tab,
+                                                Step2c (&s)[2], double& m, double& hm, const ExpConsts& kk,
+                                                int range_hint, unsigned long long out_mask) {
+    static_assert(doubled_areas<FID>(), "carried areas are doubled areas");
+    m = ha + hb;                                             // the parent's midpoint (:187)
+    hm = 0.5 * m;
+    const double mid[2] = {ha + hm, hm + hb};                // :187 for [a, m] and [m, b]
+    const double fl[2] = {fa, fm}, fr[2] = {fm, fb}, lr[2] = {lr0, lr1};
+    double wl[2], wr[2];
+    wl[0] = __fma_rn(ha, -2.0, mid[0]);                      // mid - l
+    wl[1] = mid[1] - m;
+    wr[0] = m - mid[0];                                      // r - mid
+    wr[1] = __fma_rn(hb, 2.0, -mid[1]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) asm volatile("" : "+v"(wl[k]), "+v"(wr[k]));
+    double fmid[2];
+    integrand_k<FID, 2, (f_scale<FID>() != 1.0)>(mid, fmid, tab, kk, range_hint, out_mask);   // :188
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        s[k].fmid = fmid[k];
+        s[k].l2 = (fl[k] + fmid[k]) * wl[k];                // 2 * larea, :189
+        s[k].r2 = (fmid[k] + fr[k]) * wr[k];                // 2 * rarea, :190
+        s[k].area2 = s[k].l2 + s[k].r2;
+        s[k].refine = fabs(s[k].area2 - lr[k]) > eps2;      // :191 against the carried 2 * lrarea (:185)
+    }
+}
+
 // Double-double (hi + lo) sums of the accepted areas: every leaf area enters a per-lane pair
 // exactly (Knuth's TwoSum, six flops), the pairs reduce across the wave and the workers without
 // rounding, and only the final hi + lo is rounded -- so the area is the correctly rounded sum of

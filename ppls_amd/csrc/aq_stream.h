@@ -175,6 +175,24 @@ constexpr bool OUTER_UNI = AQ_OUTER_UNI != 0;
 #define AQ_INBURST 1
 #endif
 constexpr bool INBURST = AQ_INBURST != 0;   // re-assert the outer loop's wave state uniform (k_stream)
+#ifndef AQ_PUSH_NOBR
+#define AQ_PUSH_NOBR 1
+#endif
+constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without branches (lds_push6x2)
+// Depth cap checked once per burst (r03): a round pushes every refining task's children and keeps, per
+// lane, the deepest REFINING pair it saw (masked max, as before over the popped pairs); the burst's
+// end tests that against max_depth - 1 -- one compare per burst instead of a compare, two SALU and a
+// branch per round. A burst runs at most give_rounds (<= 32) rounds, so pairs past the cap are at
+// most 32 levels deeper (max_depth <= 127: the depth byte cannot overflow), and a wave that finds the
+// cap exceeded drops its ring and cellar before anything else can see them: nothing deeper than the
+// cap ever reaches the pool or the HBM queue. The run is then invalid (ERRB_DEPTH), as before.
+#ifndef AQ_BURST_CAP
+#define AQ_BURST_CAP 1
+#endif
+#ifndef AQ_LOOPCTL
+#define AQ_LOOPCTL 1
+#endif
+constexpr bool LOOPCTL = AQ_LOOPCTL != 0;   // the burst's edge test on an opaque copy of the round count
 constexpr int PF_ISSUE = PF_LAZY ? AQ_PF_ISSUE : AQ_PF_BELOW;
 static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
 #ifndef AQ_PREFETCH
@@ -420,7 +438,8 @@ struct Acc {
     double hi, lo;                  // double-double area (aq_device.h two_sum)
     unsigned tasks, leaves, maxd;   // per lane (seeding, mixed rounds)
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
-    unsigned maxdt;                 // per lane: the deepest pair depth (dt's low byte) a round popped
+    unsigned maxdt;                 // per lane: the deepest pair depth (dt's low byte) a round popped, or
+                                    // with the per-burst cap (AQ_BURST_CAP) the deepest pair a round pushed
 };
 
 // Flush a wave's accumulators for integral `tag` and reset them: the wave's double-double area (hi
@@ -490,6 +509,13 @@ __device__ __forceinline__ double2 sload_bounds(const double2* base, int p) {
 // LDS operations it does not see -- and the "memory" clobbers keep the compiler's own LDS accesses
 // on their side of both.
 static_assert(LREC * 8 == 50 * 512, "lds_pop6 / lds_push6 assume 50 x 512 B per field");
+// AQ_POP_NOMEM: the round's pop without the "memory" clobber (it is volatile, so it stays ordered with
+// the pushes and cellar moves, all volatile asm; the compiler's own LDS accesses in a burst are reads
+// of the exp table, never written there) -- the clobber made the compiler wait for every LDS access
+// in flight before each pop
+#ifndef AQ_POP_NOMEM
+#define AQ_POP_NOMEM 0
+#endif
 __device__ __forceinline__ void lds_pop6(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
                                          unsigned& dt) {
     f64x2 ab, ff, fd;
@@ -500,7 +526,11 @@ __device__ __forceinline__ void lds_pop6(unsigned addr, double& a, double& b, do
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(ab), "=&v"(ff), "=&v"(fd)
         : "v"(addr)
+#if AQ_POP_NOMEM
+        );
+#else
         : "memory");
+#endif
     a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
     dt = (unsigned)__double_as_longlong(fd.y);
 }
@@ -513,6 +543,31 @@ __device__ __forceinline__ void lds_push6(unsigned addr, double a, double b, dou
         "ds_write2st64_b64 %0, %5, %6 offset0:200 offset1:250"
         :
         : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb), "v"(dw)
+        : "memory");
+}
+// A round's two pushes (the children pairs of the refining tasks 0 / 1) under the exec masks m0 / m1,
+// with no branch: exec is saved once, set to each mask around its three writes and restored (an empty
+// mask makes the writes no-ops). The compiler's form -- s_and_saveexec, s_cbranch_execz, s_or_b64
+// exec per push -- put two branches in every round. Every mask is a subset of the caller's exec.
+__device__ __forceinline__ void lds_push6x2(unsigned long long m0, unsigned a0, double x0, double y0, double u0,
+                                            double v0, double w0, unsigned long long m1, unsigned a1, double x1,
+                                            double y1, double u1, double v1, double w1, unsigned dt) {
+    const double dw = __longlong_as_double((long long)dt);
+    unsigned long long saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "ds_write2st64_b64 %3, %5, %6 offset1:50\n\t"
+        "ds_write2st64_b64 %3, %7, %8 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %3, %9, %15 offset0:200 offset1:250\n\t"
+        "s_mov_b64 exec, %2\n\t"
+        "ds_write2st64_b64 %4, %10, %11 offset1:50\n\t"
+        "ds_write2st64_b64 %4, %12, %13 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %4, %14, %15 offset0:200 offset1:250\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "s"(m0), "s"(m1), "v"(a0), "v"(a1), "v"(x0), "v"(y0), "v"(u0), "v"(v0), "v"(w0), "v"(x1), "v"(y1),
+          "v"(u1), "v"(v1), "v"(w1), "v"(dw)
         : "memory");
 }
 // The pipelined burst's pair registers: one slot's six fields as lds_pop6 reads them, in two steps.
@@ -714,6 +769,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
     };
     const ExpConsts kk = pinned_exp_consts();
+    // the depth cap per burst (AQ_BURST_CAP); the histogram instance keeps the per-round test
+    constexpr bool burst_cap = AQ_BURST_CAP != 0 && !HIST;
     for (;;) {
         // the wave's ring / cellar state, re-asserted uniform once per iteration: the loop's many
         // divergent lane-level blocks (copies, seeding) otherwise leave it in VGPRs, and every check
@@ -984,6 +1041,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     // a surviving position node emits its children pair (depth D + 1)
                     alive = isnode && valid && (int)d == D && dstar >= nlev && D + 1 < max_depth;
+                    // (the per-burst cap's maxdt counts pushed pairs only: the seeds' depth goes here)
+                    if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
                     if constexpr (DIAG) cp2 = clk();
                 } else {
                     for (unsigned q0 = 0; q0 < nnodes + 2; q0 += 64) {
@@ -1056,6 +1115,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                             }
                         }
                         alive = dstar >= nlev && D + 1 < max_depth;
+                        if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
                         if (alive) {
                             unsigned li = nnodes, ri = nnodes + 1;
                             for (int i = 0; i < D; ++i) {
@@ -1357,10 +1417,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
         unsigned b_r = 0;                                              // rounds run in this burst
-        bool b_go;
 #if AQ_PREBURST_WAIT
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), compiler-visible: nothing pending at the burst's header
 #endif
+        bool b_go;
+        for (;;) {   // the burst: runs of rounds (the inner loop, its exit one compare), and the cellar
+                     // moves at the window's edges between them
         do {
             // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
             //      tasks of a pair are evaluated together (two interleaved cosh chains)
@@ -1391,20 +1453,27 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
             // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
             // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
-            const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
-            const unsigned long long okm = am & dm;
-            // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
-            const unsigned long long atcap = am & ~dm;
-            if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
+            unsigned long long okm = am;
+            if constexpr (!burst_cap) {
+                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+                okm = am & dm;
+                // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
+                const unsigned long long atcap = am & ~dm;
+                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
+            }
             // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
             // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
             // counts are wave-level, the area one masked add per accepted task.
             const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
             b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
             // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-            // (doubled areas: halved at flush); the deepest pair popped, under the active mask
-            masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, dt, am);
+            // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
+            // with the per-burst depth cap, the deepest refining pair
+            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
+            const unsigned cdt = dt + 1u;                       // depth + 1, same integral
+            masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                        burst_cap ? (mask0 | mask1) : am);
             if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
                                     // takes and seeds switch the tag); checked in diagnostic builds
                 const int rtag = (int)(dt >> TAG_SHIFT);
@@ -1421,14 +1490,18 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if constexpr (DIAG) c1 = clk();
             // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
             // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
-            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
             const unsigned cnt0 = (unsigned)__popcll(mask0);
-            const unsigned cdt = dt + 1u;                       // depth + 1, same integral
-            if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
-                lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
-            }
-            if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
-                lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
+            if constexpr (PUSH_NOBR) {
+                lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
+                            mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
+                            cdt);
+            } else {
+                if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
+                    lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
+                }
+                if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
+                    lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
+                }
             }
             b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
             if constexpr (DIAG) {
@@ -1452,7 +1525,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             unsigned span_r = b_r != b_max ? b_span : 0u;
             asm("" : "+s"(span_r));
             b_go = sz - b_lo1 < span_r;
-            if (INBURST && PF_LAZY && __builtin_expect(!b_go, 0) && b_r != b_max && sz != 0u) {
+            __builtin_amdgcn_wave_barrier();
+        } while (b_go);
+            // the edge test reads b_r through an opaque copy: otherwise the compiler keeps `b_r != b_max`
+            // as a materialised lane mask across the round's select
+            unsigned b_re = b_r;
+            if constexpr (LOOPCTL) asm volatile("" : "+s"(b_re));
+            const unsigned sz = b_size;
+            if (INBURST && PF_LAZY && b_re != b_max && sz != 0u) {
                 // a cellar edge (not the give / poll round, not an empty ring): move the chunk here
                 // and go on (the cellar-full spill and the pool / queue fallbacks stay outside)
                 if (sz > (unsigned)(WCAP - 64)) {
@@ -1488,7 +1568,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
             }
             __builtin_amdgcn_wave_barrier();
-        } while (b_go);
+            if (!b_go) break;
+        }
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;
@@ -1501,6 +1582,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         acc.ut += 2u * b_n;
         acc.ul += b_n - (b_top - b_top0);
         if (b_dv) err |= ERRB_DEPTH;
+        if constexpr (burst_cap) {
+            // the per-burst depth cap: a pushed pair at depth >= max_depth means a task at the cap
+            // refined. The wave drops its ring and cellar (the run is invalid) before anything can hand
+            // the pairs on, so nothing past the cap leaves the wave (see AQ_BURST_CAP)
+            if (__builtin_expect(__ballot((acc.maxdt & 255u) >= (unsigned)max_depth) != 0ull, 0)) {
+                err |= ERRB_DEPTH;
+                top = bot;
+                ctop = 0;
+                pf_n = 0;
+            }
+        }
         mixed = b_mixed;
         __builtin_amdgcn_wave_barrier();   // reconverge before the loop latch (keeps wave state uniform)
     }

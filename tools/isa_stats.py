@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--kernel", default="_ZN2aq8k_streamILi0ELb0ELb0ELb0EEEvNS_12StreamParamsE")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--dump", action="store_true", help="print the loop body")
+    ap.add_argument("--keep", help="also write the kernel's assembly (with labels) to this file")
     a = ap.parse_args()
     d = tempfile.mkdtemp()
     out = os.path.join(d, "k.s")
@@ -60,6 +61,8 @@ def main():
     i = s.index(a.kernel + ":")
     j = s.index(".Lfunc_end", i)
     body = s[i:j].split("\n")
+    if a.keep:
+        open(a.keep, "w").write(s[i:j])
     # blocks: a label line ".LBBx_y:" with LLVM's loop comment ("Loop Header: Depth=k" or "in Loop:
     # Header=BBx_z Depth=k"); the round's loop is the innermost loop whose blocks hold the v_rcp_f64 of
     # the division, a v_mbcnt_lo and a ds_read2st64 -- counted over ALL its blocks (a rotated loop

@@ -69,21 +69,63 @@ __global__ __launch_bounds__(BLOCK) void k_step(const aq::ExpPair* __restrict__ 
     out[gid] = acc + (double)refined;
 }
 
+// The same walk with the parent's doubled areas carried in the pair (aq_device.h pair_step_carry):
+// what the step costs if the ring held two more doubles per pair.
 template <int BLOCK>
-int run(aq::ExpPair* dtab, double* dout, int cus, int blocks_per_cu, int iters) {
+__global__ __launch_bounds__(BLOCK) void k_step_carry(const aq::ExpPair* __restrict__ gtab, double* out, int iters,
+                                                      double eps2) {
+    __shared__ aq::ExpEntry tab[128];
+    aq::stage_exp_table(tab, gtab);
+    __syncthreads();
+    const aq::ExpConsts kk = aq::pinned_exp_consts();
+    const unsigned gid = blockIdx.x * BLOCK + threadIdx.x;
+    const double a0 = 0.4 + 4.0 * (double)(gid % 4093) / 4093.0, b0 = a0 + 0.5;
+    auto F16 = [&](double x) { return 16.0 * aq::integrand<aq::F_COSH4>(x, tab); };
+    const double s_ha = 0.5 * a0, s_hb = 0.5 * b0, s_fa = F16(a0), s_fm = F16(0.5 * (a0 + b0)), s_fb = F16(b0);
+    const double s_m = s_ha + s_hb;
+    const double s_l2 = (s_fa + s_fm) * (s_m - a0), s_r2 = (s_fm + s_fb) * (b0 - s_m);
+    double ha = s_ha, hb = s_hb, fa = s_fa, fm = s_fm, fb = s_fb, l2 = s_l2, r2 = s_r2;
+    double acc = 0.0;
+    unsigned refined = 0;
+    int lev = 0;
+#pragma unroll 1
+    for (int it = 0; it < iters; ++it) {
+        aq::Step2c st[2];
+        double m, hm;
+        aq::pair_step_carry<aq::F_COSH4>(ha, hb, fa, fm, fb, l2, r2, eps2, tab, st, m, hm, kk, 2, 0ull);
+        if (!st[0].refine) acc += st[0].area2;
+        if (!st[1].refine) acc += st[1].area2;
+        refined += (unsigned)st[0].refine + (unsigned)st[1].refine;
+        const bool right = !st[0].refine;
+        const double nha = right ? hm : ha, nhb = right ? hb : hm;
+        const double nfa = right ? fm : fa, nfm = right ? st[1].fmid : st[0].fmid, nfb = right ? fb : fm;
+        const double nl2 = right ? st[1].l2 : st[0].l2, nr2 = right ? st[1].r2 : st[0].r2;
+        if (++lev == 24) {
+            lev = 0;
+            ha = s_ha; hb = s_hb; fa = s_fa; fm = s_fm; fb = s_fb; l2 = s_l2; r2 = s_r2;
+        } else {
+            ha = nha; hb = nhb; fa = nfa; fm = nfm; fb = nfb; l2 = nl2; r2 = nr2;
+        }
+    }
+    out[gid] = acc + (double)refined;
+}
+
+template <int BLOCK>
+int run(aq::ExpPair* dtab, double* dout, int cus, int blocks_per_cu, int iters, bool carry = false) {
     const int grid = cus * blocks_per_cu;
     hipFuncAttributes attr;
-    CHECK(hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&k_step<BLOCK>)));
+    auto kern = carry ? &k_step_carry<BLOCK> : &k_step<BLOCK>;
+    CHECK(hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(kern)));
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
     const double eps2 = 1e-10 * 32.0;   // the bench's eps on doubled areas of 16 F
-    hipLaunchKernelGGL((k_step<BLOCK>), dim3(grid), dim3(BLOCK), 0, 0, dtab, dout, 16, eps2);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, 0, dtab, dout, 16, eps2);
     CHECK(hipDeviceSynchronize());
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
         CHECK(hipEventRecord(a));
-        hipLaunchKernelGGL((k_step<BLOCK>), dim3(grid), dim3(BLOCK), 0, 0, dtab, dout, iters, eps2);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), 0, 0, dtab, dout, iters, eps2);
         CHECK(hipEventRecord(b));
         CHECK(hipEventSynchronize(b));
         float ms = 0;
@@ -92,9 +134,9 @@ int run(aq::ExpPair* dtab, double* dout, int cus, int blocks_per_cu, int iters) 
     }
     const double tasks = 2.0 * (double)grid * BLOCK * iters;
     const double rate = tasks / (best * 1e-3);
-    printf("{\"block\": %d, \"blocks_per_cu\": %d, \"waves_per_simd\": %d, \"vgprs\": %d, \"ms\": %.3f, "
+    printf("{\"carry\": %d, \"block\": %d, \"blocks_per_cu\": %d, \"waves_per_simd\": %d, \"vgprs\": %d, \"ms\": %.3f, "
            "\"tasks_per_s\": %.4e, \"frac_fp64_38flop\": %.4f}\n",
-           BLOCK, blocks_per_cu, BLOCK * blocks_per_cu / 256, attr.numRegs, best, rate, 38.0 * rate / 78.6e12);
+           (int)carry, BLOCK, blocks_per_cu, BLOCK * blocks_per_cu / 256, attr.numRegs, best, rate, 38.0 * rate / 78.6e12);
     return 0;
 }
 
@@ -113,5 +155,8 @@ int main() {
     run<768>(dtab, dout, cus, 1, it);    // 3: the persistent kernel's occupancy
     run<1024>(dtab, dout, cus, 1, it);   // 4
     run<1024>(dtab, dout, cus, 2, it);   // 8
+    run<512>(dtab, dout, cus, 1, it, true);    // carried parent areas (pair_step_carry)
+    run<768>(dtab, dout, cus, 1, it, true);
+    run<1024>(dtab, dout, cus, 1, it, true);
     return 0;
 }
