@@ -179,6 +179,9 @@ constexpr bool INBURST = AQ_INBURST != 0;   // re-assert the outer loop's wave s
 #define AQ_PUSH_NOBR 1
 #endif
 constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without branches (lds_push6x2)
+#ifndef AQ_ONE_WINDOW
+#define AQ_ONE_WINDOW 1
+#endif
 // Depth cap checked once per burst (r03): a round pushes every refining task's children and keeps, per
 // lane, the deepest REFINING pair it saw (masked max, as before over the popped pairs); the burst's
 // end tests that against max_depth - 1 -- one compare per burst instead of a compare, two SALU and a
@@ -192,7 +195,19 @@ constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without 
 #ifndef AQ_LOOPCTL
 #define AQ_LOOPCTL 1
 #endif
-constexpr bool LOOPCTL = AQ_LOOPCTL != 0;   // the burst's edge test on an opaque copy of the round count
+constexpr bool LOOPCTL = AQ_LOOPCTL != 0;
+// Full rounds (r03): while the ring holds >= 64 pairs a round pops 64 and every lane is active, so its
+// masks need no active-lane ballot or AND, its pair count no min and its task count no add (counted
+// per run of full rounds); the round is compiled twice, and the burst runs full rounds in an inner
+// loop whose window keeps the ring at >= 64 pairs.
+#ifndef AQ_FULLR
+#define AQ_FULLR 1
+#endif
+constexpr bool FULLR = AQ_FULLR != 0;
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};   // the burst's edge test on an opaque copy of the round count
 constexpr int PF_ISSUE = PF_LAZY ? AQ_PF_ISSUE : AQ_PF_BELOW;
 static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
 #ifndef AQ_PREFETCH
@@ -570,6 +585,62 @@ __device__ __forceinline__ void lds_push6x2(unsigned long long m0, unsigned a0, 
           "v"(u1), "v"(v1), "v"(w1), "v"(dw)
         : "memory");
 }
+// masked_acc3 and lds_push6x2 in ONE exec window (AQ_ONE_WINDOW): exec saved once and restored once
+// for the round's two masked area adds, its masked depth max and its two pushes (two SALU fewer).
+// EXEC_FULL: the caller's exec is all 64 lanes (a full round), restored as -1 with nothing saved.
+template <bool EXEC_FULL = false>
+__device__ __forceinline__ void acc3_push6x2(double& hi, double ar0, unsigned long long l0m, double ar1,
+                                             unsigned long long l1m, unsigned& mx, unsigned v, unsigned long long mm,
+                                             unsigned long long m0, unsigned a0, double x0, double y0, double u0,
+                                             double v0, double w0, unsigned long long m1, unsigned a1, double x1,
+                                             double y1, double u1, double v1, double w1, unsigned dt) {
+    const double dw = __longlong_as_double((long long)dt);
+    unsigned long long saved = 0;
+    if constexpr (EXEC_FULL) {
+        asm volatile(
+            "s_mov_b64 exec, %5\n\t"
+            "v_add_f64 %0, %0, %2\n\t"
+            "s_mov_b64 exec, %6\n\t"
+            "v_add_f64 %0, %0, %3\n\t"
+            "s_mov_b64 exec, %7\n\t"
+            "v_max_u32_sdwa %1, %1, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
+            "s_mov_b64 exec, %8\n\t"
+            "ds_write2st64_b64 %10, %12, %13 offset1:50\n\t"
+            "ds_write2st64_b64 %10, %14, %15 offset0:100 offset1:150\n\t"
+            "ds_write2st64_b64 %10, %16, %22 offset0:200 offset1:250\n\t"
+            "s_mov_b64 exec, %9\n\t"
+            "ds_write2st64_b64 %11, %17, %18 offset1:50\n\t"
+            "ds_write2st64_b64 %11, %19, %20 offset0:100 offset1:150\n\t"
+            "ds_write2st64_b64 %11, %21, %22 offset0:200 offset1:250\n\t"
+            "s_mov_b64 exec, -1"
+            : "+v"(hi), "+v"(mx)
+            : "v"(ar0), "v"(ar1), "v"(v), "s"(l0m), "s"(l1m), "s"(mm), "s"(m0), "s"(m1), "v"(a0), "v"(a1), "v"(x0),
+              "v"(y0), "v"(u0), "v"(v0), "v"(w0), "v"(x1), "v"(y1), "v"(u1), "v"(v1), "v"(w1), "v"(dw)
+            : "memory");
+        return;
+    }
+    asm volatile(
+        "s_mov_b64 %2, exec\n\t"
+        "s_mov_b64 exec, %6\n\t"
+        "v_add_f64 %0, %0, %3\n\t"
+        "s_mov_b64 exec, %7\n\t"
+        "v_add_f64 %0, %0, %4\n\t"
+        "s_mov_b64 exec, %8\n\t"
+        "v_max_u32_sdwa %1, %1, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
+        "s_mov_b64 exec, %9\n\t"
+        "ds_write2st64_b64 %11, %13, %14 offset1:50\n\t"
+        "ds_write2st64_b64 %11, %15, %16 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %11, %17, %23 offset0:200 offset1:250\n\t"
+        "s_mov_b64 exec, %10\n\t"
+        "ds_write2st64_b64 %12, %18, %19 offset1:50\n\t"
+        "ds_write2st64_b64 %12, %20, %21 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %12, %22, %23 offset0:200 offset1:250\n\t"
+        "s_mov_b64 exec, %2"
+        : "+v"(hi), "+v"(mx), "=&s"(saved)
+        : "v"(ar0), "v"(ar1), "v"(v), "s"(l0m), "s"(l1m), "s"(mm), "s"(m0), "s"(m1), "v"(a0), "v"(a1), "v"(x0),
+          "v"(y0), "v"(u0), "v"(v0), "v"(w0), "v"(x1), "v"(y1), "v"(u1), "v"(v1), "v"(w1), "v"(dw)
+        : "memory");
+}
 // The pipelined burst's pair registers: one slot's six fields as lds_pop6 reads them, in two steps.
 // lds_issue6 only ISSUES the three ds_read2st64_b64; lds_wait6 waits for every outstanding LDS access
 // and is the point from which the registers hold the pair -- nothing may read them before (the
@@ -771,6 +842,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const ExpConsts kk = pinned_exp_consts();
     // the depth cap per burst (AQ_BURST_CAP); the histogram instance keeps the per-round test
     constexpr bool burst_cap = AQ_BURST_CAP != 0 && !HIST;
+    // the round's accumulations and pushes in one exec window (not in the histogram / diagnostic
+    // instances, whose per-round extras sit between them)
+    constexpr bool one_window = AQ_ONE_WINDOW != 0 && PUSH_NOBR && !HIST && !DIAG;
     for (;;) {
         // the wave's ring / cellar state, re-asserted uniform once per iteration: the loop's many
         // divergent lane-level blocks (copies, seeding) otherwise leave it in VGPRs, and every check
@@ -1403,6 +1477,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // WCAP - 64 (near overflow), or hi = lo while a prefetch is in flight (one round only).
         // One subtract and one compare per round, and one compare for the round counter.
         unsigned b_lo1, b_span;
+        unsigned b_lo1f, b_spanf;   // the full rounds' window: lo raised to 63 (a full round needs 64 pairs)
         auto window = [&]() {
             if constexpr (PF_LAZY) {
                 // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar
@@ -1413,126 +1488,159 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
                 b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
             }
+            b_lo1f = max(b_lo1, 64u);
+            b_spanf = b_span == 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1f;
         };
         window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
-        unsigned b_r = 0;                                              // rounds run in this burst
+        unsigned b_rem = b_max;   // rounds left up to the give / poll round (counted down: no copy of a
+                                  // round counter per round)
 #if AQ_PREBURST_WAIT
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), compiler-visible: nothing pending at the burst's header
 #endif
+        // one round: FULL = the ring holds >= 64 pairs (every lane pops one)
+        auto round_body = [&](auto full) __attribute__((always_inline)) {
+            constexpr bool FULL = decltype(full)::value;
+                // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
+                //      tasks of a pair are evaluated together (two interleaved cosh chains)
+                unsigned long long c0 = 0, c1 = 0;
+                if constexpr (DIAG) c0 = clk();
+                const unsigned n = FULL ? 64u : min(b_size, 64u);
+                const unsigned b0 = b_top - n;
+                const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
+                // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
+                double pa, pb, pfa, pfm, pfb;
+                unsigned dt;
+                lds_pop6(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dt);
+                Step2 st[2];
+                // both midpoints lie in [pa, pb]: one range test for the pair
+                // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
+                // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
+                // compiler turns the byte test into an and plus a compare
+                unsigned long long nospan = 0ull;
+                if constexpr (FID == F_COSH4)
+                    asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
+                // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
+                // measured 0.9 % slower)
+                // a full round (FULL: 64 pairs or more in the ring) has every lane active: its masks need no
+                // active-lane ballot, and no AND with one
+                const unsigned long long am = FULL ? ~0ull : __ballot(lane < n);
+                // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
+                double pm, hm;
+                pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+                // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
+                // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
+                // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
+                const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
+                unsigned long long okm = am;
+                if constexpr (!burst_cap) {
+                    const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+                    okm = am & dm;
+                    // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
+                    const unsigned long long atcap = am & ~dm;
+                    if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
+                }
+                // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
+                // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
+                // counts are wave-level, the area one masked add per accepted task.
+                const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
+                if constexpr (!FULL) b_n += n;   // tasks 2n (full rounds: counted per run of rounds); accepted:
+                                                 // counted once per burst from the ring's growth (below)
+                // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
+                // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
+                // with the per-burst depth cap, the deepest refining pair
+                const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
+                const unsigned cdt = dt + 1u;                       // depth + 1, same integral
+                if constexpr (!one_window)
+                    masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                                burst_cap ? (mask0 | mask1) : am);
+                if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
+                                        // takes and seeds switch the tag); checked in diagnostic builds
+                    const int rtag = (int)(dt >> TAG_SHIFT);
+                    b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
+                }
+                if (HIST) {
+                    const unsigned d = dt & 255u;
+                    if (__builtin_amdgcn_inverse_ballot_w64(am)) {
+                        atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                        const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
+                        if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+                    }
+                }
+                if constexpr (DIAG) c1 = clk();
+                // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
+                // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
+                const unsigned cnt0 = (unsigned)__popcll(mask0);
+                if constexpr (one_window) {
+                    acc3_push6x2<FULL>(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                                 burst_cap ? (mask0 | mask1) : am,
+                                 mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
+                                 mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
+                                 cdt);
+                } else if constexpr (PUSH_NOBR) {
+                    lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
+                                mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
+                                cdt);
+                } else {
+                    if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
+                        lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
+                    }
+                    if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
+                        lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
+                    }
+                }
+                b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
+                if constexpr (DIAG) {
+                    if (lane == 0) {
+                        const unsigned long long c2 = clk();
+                        atomicAdd(&s_dg[DG_ROUNDS], 1ull);
+                        atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
+                        atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
+                        atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
+                        atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
+                        atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
+                    }
+                    const unsigned nt = 2u * n;
+                    if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
+                }
+        };
         bool b_go;
-        for (;;) {   // the burst: runs of rounds (the inner loop, its exit one compare), and the cellar
-                     // moves at the window's edges between them
-        do {
-            // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
-            //      tasks of a pair are evaluated together (two interleaved cosh chains)
-            unsigned long long c0 = 0, c1 = 0;
-            if constexpr (DIAG) c0 = clk();
-            const unsigned n = min(b_size, 64u);
-            const unsigned b0 = b_top - n;
-            const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
-            const bool act = lane < n;
-            // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
-            double pa, pb, pfa, pfm, pfb;
-            unsigned dt;
-            lds_pop6(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dt);
-            Step2 st[2];
-            // both midpoints lie in [pa, pb]: one range test for the pair
-            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
-            // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
-            // compiler turns the byte test into an and plus a compare
-            unsigned long long nospan = 0ull;
-            if constexpr (FID == F_COSH4)
-                asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
-            // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
-            // measured 0.9 % slower)
-            const unsigned long long am = __ballot(act);
-            // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
-            double pm, hm;
-            pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
-            // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
-            // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
-            // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
-            const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
-            unsigned long long okm = am;
-            if constexpr (!burst_cap) {
-                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
-                okm = am & dm;
-                // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
-                const unsigned long long atcap = am & ~dm;
-                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
-            }
-            // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
-            // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
-            // counts are wave-level, the area one masked add per accepted task.
-            const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
-            b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
-            // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-            // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
-            // with the per-burst depth cap, the deepest refining pair
-            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-            const unsigned cdt = dt + 1u;                       // depth + 1, same integral
-            masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
-                        burst_cap ? (mask0 | mask1) : am);
-            if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
-                                    // takes and seeds switch the tag); checked in diagnostic builds
-                const int rtag = (int)(dt >> TAG_SHIFT);
-                b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
-            }
-            if (HIST) {
-                const unsigned d = dt & 255u;
-                if (__builtin_amdgcn_inverse_ballot_w64(am)) {
-                    atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
-                    const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
-                    if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
-                }
-            }
-            if constexpr (DIAG) c1 = clk();
-            // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
-            // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
-            const unsigned cnt0 = (unsigned)__popcll(mask0);
-            if constexpr (PUSH_NOBR) {
-                lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
-                            mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
-                            cdt);
+        for (;;) {   // the burst: runs of rounds (the inner loops, their exits one compare each), and the
+                     // cellar moves at the window's edges between them
+        for (;;) {
+            if (FULLR && b_size >= 64u) {
+                // full rounds while the window holds AND the ring keeps >= 64 pairs (lo raised to 64)
+                const unsigned r_in = b_rem;
+                unsigned szf, span_f;
+                do {
+                    --b_rem;   // (first: the old count is dead before the round, so no copy at the latch)
+                    round_body(BoolC<true>{});
+                    szf = b_top - b_bot;
+                    span_f = b_rem != 0u ? b_spanf : 0u;
+                    asm("" : "+s"(span_f));
+                    __builtin_amdgcn_wave_barrier();
+                } while (szf - b_lo1f < span_f);
+                b_n += 64u * (r_in - b_rem);
+                b_size = szf;
             } else {
-                if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
-                    lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
-                }
-                if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
-                    lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
-                }
+                round_body(BoolC<false>{});
+                b_size = b_top - b_bot;
+                --b_rem;
             }
-            b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
-            if constexpr (DIAG) {
-                if (lane == 0) {
-                    const unsigned long long c2 = clk();
-                    atomicAdd(&s_dg[DG_ROUNDS], 1ull);
-                    atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
-                    atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
-                    atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
-                    atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
-                    atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
-                }
-                const unsigned nt = 2u * n;
-                if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
-            }
-            const unsigned sz = b_top - b_bot;
-            b_size = sz;
-            ++b_r;
             // one compare: the give / poll round closes the size window (opaque, so the compiler does
             // not split it back into two conditions joined by SALU selects)
-            unsigned span_r = b_r != b_max ? b_span : 0u;
+            unsigned span_r = b_rem != 0u ? b_span : 0u;
             asm("" : "+s"(span_r));
-            b_go = sz - b_lo1 < span_r;
+            b_go = b_size - b_lo1 < span_r;
             __builtin_amdgcn_wave_barrier();
-        } while (b_go);
-            // the edge test reads b_r through an opaque copy: otherwise the compiler keeps `b_r != b_max`
+            if (!b_go) break;
+        }
+            // the edge test reads b_rem through an opaque copy: otherwise the compiler keeps `b_rem != 0`
             // as a materialised lane mask across the round's select
-            unsigned b_re = b_r;
+            unsigned b_re = b_rem;
             if constexpr (LOOPCTL) asm volatile("" : "+s"(b_re));
             const unsigned sz = b_size;
-            if (INBURST && PF_LAZY && b_re != b_max && sz != 0u) {
+            if (INBURST && PF_LAZY && b_re != 0u && sz != 0u) {
                 // a cellar edge (not the give / poll round, not an empty ring): move the chunk here
                 // and go on (the cellar-full spill and the pool / queue fallbacks stay outside)
                 if (sz > (unsigned)(WCAP - 64)) {
@@ -1573,7 +1681,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;
-        b_poll += b_r - 1u;   // every round but the burst's last advances the give / poll counter
+        b_poll += (b_max - b_rem) - 1u;   // every round but the burst's last advances the give / poll counter
         top = b_top;
         poll_ctr = b_poll;
         // every refining task pushed one pair, so pushes = (b_top - b_top0) + b_n and the accepted

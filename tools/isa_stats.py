@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--kernel", default="_ZN2aq8k_streamILi0ELb0ELb0ELb0EEEvNS_12StreamParamsE")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--dump", action="store_true", help="print the loop body")
+    ap.add_argument("--first-backedge", action="store_true",
+                    help="bottom-tested loop: count up to the first conditional back-edge")
     ap.add_argument("--keep", help="also write the kernel's assembly (with labels) to this file")
     a = ap.parse_args()
     d = tempfile.mkdtemp()
@@ -106,8 +108,14 @@ def main():
     hi = h
     while hi + 1 < len(blocks) and inloop(blocks[hi + 1], best):
         hi += 1
-    heads = "|".join(re.escape(b[0]) for b in blocks[lo:h + 1])   # the latch run and the header
-    last = max(i for i in range(h, hi + 1) if any(re.search(r"s_(cbranch_\w+|branch)\s+(" + heads + r")\b", x) for x in blocks[i][3]))
+    heads = "|".join(re.escape(b[0]) for b in blocks[(h if a.first_backedge else lo):h + 1])   # the latch run and the header
+    backs = [i for i in range(h, hi + 1) if any(re.search(r"s_(cbranch_\w+|branch)\s+(" + heads + r")\b", x) for x in blocks[i][3])]
+    # a bottom-tested loop (its back-edge a conditional branch to the header) ends at its FIRST back-edge;
+    # blocks after it that also branch back are out-of-line paths (the cosh_glibc fallback)
+    first_cond = [i for i in backs if any(re.search(r"s_cbranch_\w+\s+(" + heads + r")\b", x) for x in blocks[i][3])]
+    last = min(first_cond) if (a.first_backedge and first_cond) else max(backs)
+    if a.first_backedge:
+        lo = h
     seg = [x for b in blocks[lo:last + 1] for x in [b[0] + ":"] + b[3]]
     seg = [x for x in seg if re.match(r"^\s+[a-z]", x) and not x.strip().startswith(";")]
     counts = {}
