@@ -72,7 +72,9 @@ def cpu_baseline(eps, target_s=12.0):
                     "host_cpus": ncpu, "kind": "port",
                     "sample": f"{runs} full integrals (cosh4 [0,5], eps={eps}) by oracle/aq_bag -- the reference's "
                               f"farmer/worker bag of tasks on threads, farmer + {nprocs - 1} workers on {nprocs} of "
-                              f"this host's {ncpu} CPUs -- {t_total:.1f} s wall"}
+                              f"this host's {ncpu} CPUs -- {t_total:.1f} s wall; the single farmer thread "
+                              f"(one message round trip per task, aquadPartA.c:145-171) bounds it, not the "
+                              f"core count"}
         except Exception as e:
             print(f"cpu_baseline: oracle/aq_bag unusable ({e}); timing the sequential oracle", file=sys.stderr)
     from oracle import pyoracle as O

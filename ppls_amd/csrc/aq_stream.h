@@ -179,6 +179,9 @@ constexpr bool INBURST = AQ_INBURST != 0;   // re-assert the outer loop's wave s
 #define AQ_PUSH_NOBR 1
 #endif
 constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without branches (lds_push6x2)
+#ifndef AQ_PRO_OVERLAP
+#define AQ_PRO_OVERLAP 1   // the prologue's exp-table loads overlap the rings' set-up (k_stream)
+#endif
 #ifndef AQ_ONE_WINDOW
 #define AQ_ONE_WINDOW 1
 #endif
@@ -549,6 +552,22 @@ __device__ __forceinline__ void lds_pop6(unsigned addr, double& a, double& b, do
     a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
     dt = (unsigned)__double_as_longlong(fd.y);
 }
+// ... returning the pair word as the raw 8-byte field (its high half is zero): the round pushes
+// word + 1 (one 64-bit add) with no separate zero for the high half
+__device__ __forceinline__ void lds_pop6w(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
+                                          unsigned long long& dtw) {
+    f64x2 ab, ff, fd;
+    asm volatile(
+        "ds_read2st64_b64 %0, %3 offset1:50\n\t"
+        "ds_read2st64_b64 %1, %3 offset0:100 offset1:150\n\t"
+        "ds_read2st64_b64 %2, %3 offset0:200 offset1:250\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(ab), "=&v"(ff), "=&v"(fd)
+        : "v"(addr)
+        : "memory");
+    a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
+    dtw = (unsigned long long)__double_as_longlong(fd.y);
+}
 __device__ __forceinline__ void lds_push6(unsigned addr, double a, double b, double fa, double fm, double fb,
                                           unsigned dt) {
     const double dw = __longlong_as_double((long long)dt);
@@ -593,8 +612,8 @@ __device__ __forceinline__ void acc3_push6x2(double& hi, double ar0, unsigned lo
                                              unsigned long long l1m, unsigned& mx, unsigned v, unsigned long long mm,
                                              unsigned long long m0, unsigned a0, double x0, double y0, double u0,
                                              double v0, double w0, unsigned long long m1, unsigned a1, double x1,
-                                             double y1, double u1, double v1, double w1, unsigned dt) {
-    const double dw = __longlong_as_double((long long)dt);
+                                             double y1, double u1, double v1, double w1, unsigned long long dtw) {
+    const double dw = __longlong_as_double((long long)dtw);
     unsigned long long saved = 0;
     if constexpr (EXEC_FULL) {
         asm volatile(
@@ -727,7 +746,22 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned pr_base = (unsigned)(uintptr_t)s_pr;   // LDS byte offset of the pair block (low word of its flat address)
     const unsigned long long t_entry = DIAG ? rtc() : 0ull;
+#if AQ_PRO_OVERLAP
+    // the exp table's global loads go out first and land in LDS after the other set-up stores (the
+    // rings' harmless pairs among them): their latency, a cold HBM read at every launch, overlaps
+    // the set-up instead of preceding it
+    ExpPair tv{};
+    if (tid < 128u) tv = P.gtab[tid];
+    {
+        const unsigned b0 = (tid >> 6) * WCAP;
+        for (unsigned i = lane_id(); i < (unsigned)WCAP; i += 64) {
+            const unsigned j = b0 + i;
+            s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
+        }
+    }
+#else
     stage_exp_table(tab, P.gtab);
+#endif
     if (bid == 0)
         for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
     if (tid == 0) {
@@ -740,6 +774,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
+#if AQ_PRO_OVERLAP
+    if (tid < 128u) {
+        tab[tid].tail_bits = tv.tail_bits;
+        tab[tid].sbits = tv.sbits;
+    }
+#endif
     __syncthreads();   // the only workgroup barrier before the exit
     if constexpr (DIAG) { if (tid == 0) s_dg[DG_T_INIT] = rtc(); }
 
@@ -781,9 +821,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
     Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u, 0u};
     // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
-    for (unsigned i = lane; i < (unsigned)WCAP; i += 64) {
-        const unsigned j = base + i;
-        s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
+    if constexpr (!AQ_PRO_OVERLAP) {
+        for (unsigned i = lane; i < (unsigned)WCAP; i += 64) {
+            const unsigned j = base + i;
+            s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
+        }
     }
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
@@ -1510,8 +1552,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
                 // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
                 double pa, pb, pfa, pfm, pfb;
-                unsigned dt;
-                lds_pop6(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dt);
+                unsigned long long dtw;   // the pair word's 8-byte field (dt in its low half)
+                lds_pop6w(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dtw);
+                const unsigned dt = (unsigned)dtw;
                 Step2 st[2];
                 // both midpoints lie in [pa, pb]: one range test for the pair
                 // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
@@ -1550,7 +1593,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
                 // with the per-burst depth cap, the deepest refining pair
                 const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-                const unsigned cdt = dt + 1u;                       // depth + 1, same integral
+                const unsigned long long cdtw = dtw + 1ull;         // depth + 1, same integral
+                const unsigned cdt = (unsigned)cdtw;
                 if constexpr (!one_window)
                     masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
                                 burst_cap ? (mask0 | mask1) : am);
@@ -1576,7 +1620,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                                  burst_cap ? (mask0 | mask1) : am,
                                  mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
                                  mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
-                                 cdt);
+                                 cdtw);
                 } else if constexpr (PUSH_NOBR) {
                     lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
                                 mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,

@@ -212,6 +212,9 @@ constexpr int LEVEL_R = AQ_LEVEL_R;
 #define AQ_LEVEL_T 256
 #endif
 constexpr int LEVEL_T = AQ_LEVEL_T;
+#ifndef AQ_LEVEL_HOIST
+#define AQ_LEVEL_HOIST 1
+#endif
 constexpr int LEVEL_NW = LEVEL_T / 64;
 
 template <int FID>
@@ -228,23 +231,37 @@ __global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ 
     __shared__ double s_h[LEVEL_NW], s_l[LEVEL_NW];
     __shared__ unsigned s_t[LEVEL_NW], s_a[LEVEL_NW], s_e[LEVEL_NW];
     __shared__ unsigned s_wc[2][LEVEL_NW], s_base[2];
+    const unsigned chunk = (unsigned)LEVEL_T * R;
+    // the first chunk's records are requested BEFORE the exp table is staged (AQ_LEVEL_HOIST): a block
+    // of a wide level runs one chunk, and the table's global read (then the barrier) had preceded every
+    // record load, adding its latency to every block's
+    Rec rn[R];
+    bool an[R];
+    auto load_chunk = [&](unsigned base) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const unsigned i = base + (unsigned)k * (unsigned)LEVEL_T + threadIdx.x;
+            an[k] = i < n_in;
+            rn[k] = an[k] ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
+        }
+    };
+    if (AQ_LEVEL_HOIST && blockIdx.x * chunk < n_in) load_chunk(blockIdx.x * chunk);
     stage_exp_table(tab, gtab);
     __syncthreads();
     double hi = 0.0, lo = 0.0;
     unsigned tasks = 0, leaves = 0, err = 0;
     const unsigned w = threadIdx.x >> 6;
-    const unsigned chunk = (unsigned)LEVEL_T * R;
     unsigned parity = 0;
     // the loop bound depends on blockIdx only: every thread of the block runs every chunk (barriers)
     for (unsigned base = blockIdx.x * chunk; base < n_in; base += gridDim.x * chunk, parity ^= 1u) {
         Rec rc[R];
         bool active[R];
         double x[R], f[R];
+        if (!AQ_LEVEL_HOIST || base != blockIdx.x * chunk) load_chunk(base);
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-            const unsigned i = base + (unsigned)k * (unsigned)LEVEL_T + threadIdx.x;
-            active[k] = i < n_in;
-            rc[k] = active[k] ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
+            active[k] = an[k];
+            rc[k] = rn[k];
             x[k] = (rc[k].l + rc[k].r) / 2;                              // :187
         }
         integrand_k<FID, R>(x, f, tab);                                  // :188

@@ -56,6 +56,11 @@ def main():
     if ok.any():
         out["t_first_lead_us_q0_50_90_100"] = q((lead[ok] - t0) / 100.0)
     out["t_wait_us_per_wg_q"] = q(col["t_wait"] / 100.0)
+    if "cu" in col:   # start and exit by XCD (the CU slot's bits 8-10)
+        xcc = col["cu"].astype(np.int64) >> 8
+        out["t_start_us_by_xcd_min_max"] = {int(x): [round(float(us("t_start")[xcc == x].min()), 2),
+                                                     round(float(us("t_start")[xcc == x].max()), 2)] for x in np.unique(xcc)}
+        out["t_seeded_us_by_xcd_max"] = {int(x): round(float(us("t_seeded")[xcc == x].max()), 2) for x in np.unique(xcc)}
     for k in ("rounds", "seeds", "seed_calls", "active_lanes", "c_seed", "c_seed_pass1", "c_seed_pass2", "c_seed_resolve", "c_p1_class", "c_p1_walk", "c_p1_f", "c_loop", "c_round", "leads"):
         if k in col:
             out[k + "_q0_50_90_100"] = q(col[k])

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Kernel-trace A/B of library variants over the frontier engine (bench_frontier.py cosh12), repo root
-# on the GPU box: every ppls_amd/_build/libaquad_*.so, then per-level durations via profile_frontier.py
+# on the GPU box: every ppls_amd/_build/${AB_GLOB:-libaquad_*.so}, then per-level durations via profile_frontier.py
 #   tools/frontier_ab.sh <tag>   -> gpurun_out/front_ab_<tag>/<variant>/{bench.json, levels.json}
 set -uo pipefail
 TAG=${1:?tag}
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp
-for so in $ROOT/ppls_amd/_build/libaquad_*.so; do
+for so in $ROOT/ppls_amd/_build/${AB_GLOB:-libaquad_*.so}; do
   v=$(basename "$so" .so)
   D=$ROOT/gpurun_out/front_ab_$TAG/$v
   mkdir -p $D

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session of several measurements, each under its own time limit; a failing step ends the
+# script (no later GPU step runs after a fault). Output under gpurun_out/<tag>/.
+#   tools/gpu_session.sh <tag> [steps...]   steps: tests ubench ab front bench12 bench lone diag smoke
+#   (AB_GLOB_K / AB_GLOB_F: the library variants the k_stream / frontier A/Bs take)
+set -o pipefail
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() {   # name seconds command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  tail -4 "$OUT/$name.out"
+  if [ $rc -ne 0 ]; then echo "!! $name rc=$rc"; tail -20 "$OUT/$name.err"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    tests)   run gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    ubench)  run ubench_launch 60 tools/ubench_launch && run ubench_step 120 tools/ubench_step ;;
+    ab)      ROUNDS=${ROUNDS:-3} AB_GLOB=${AB_GLOB_K:-libaquad_*.so} run ab 900 bash tools/ab.sh "$TAG" ;;
+    front)   AB_GLOB=${AB_GLOB_F:-libaquad_*.so} run front 900 bash tools/frontier_ab.sh "$TAG" ;;
+    bench)   run bench 400 python bench.py ;;
+    bench12) run bench12 400 python bench.py --eps 1e-12 --batch 4096 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    lone)    run lone 120 python tools/try_single.py ;;
+    diag)    run diag_1e10 120 python tools/diag_single.py --eps 1e-10 && run diag_1task 120 python tools/diag_single.py --eps 1e30 ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done ($(date +%T))"
