@@ -183,7 +183,7 @@ constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without 
 #define AQ_PRO_OVERLAP 1   // the prologue's exp-table loads overlap the rings' set-up (k_stream)
 #endif
 #ifndef AQ_ONE_WINDOW
-#define AQ_ONE_WINDOW 1
+#define AQ_ONE_WINDOW 0   // r03 A/B (profiles/r03q/ab.txt): 2 SALU fewer per round, 0.6 % SLOWER -- off
 #endif
 // Depth cap checked once per burst (r03): a round pushes every refining task's children and keeps, per
 // lane, the deepest REFINING pair it saw (masked max, as before over the popped pairs); the burst's
@@ -204,7 +204,7 @@ constexpr bool LOOPCTL = AQ_LOOPCTL != 0;
 // per run of full rounds); the round is compiled twice, and the burst runs full rounds in an inner
 // loop whose window keeps the ring at >= 64 pairs.
 #ifndef AQ_FULLR
-#define AQ_FULLR 1
+#define AQ_FULLR 0   // r03 A/B (profiles/r03q/ab.txt): 7 instructions fewer per full round, 0.9 % SLOWER -- off
 #endif
 constexpr bool FULLR = AQ_FULLR != 0;
 template <bool B>

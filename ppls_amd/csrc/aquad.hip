@@ -213,7 +213,7 @@ constexpr int LEVEL_R = AQ_LEVEL_R;
 #endif
 constexpr int LEVEL_T = AQ_LEVEL_T;
 #ifndef AQ_LEVEL_HOIST
-#define AQ_LEVEL_HOIST 1
+#define AQ_LEVEL_HOIST 0   // r03 A/B (profiles/r03q/front_ab.txt): widest level 32.4 -> 35.4 us with it -- off
 #endif
 constexpr int LEVEL_NW = LEVEL_T / 64;
 

@@ -26,6 +26,8 @@ for step in "$@"; do
     lone)    run lone 120 python tools/try_single.py ;;
     diag)    run diag_1e10 120 python tools/diag_single.py --eps 1e-10 && run diag_1task 120 python tools/diag_single.py --eps 1e30 ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    xcd)     run xcd_start 120 python tools/xcd_start.py ;;
+    prof)    run prof 1000 bash tools/profile_round.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
