@@ -291,6 +291,9 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
         e[k] = tab[ki[k] & 127];
         if (CHECK) out |= !cosh_main_range(x[k]);
     }
+#if defined(AQ_SETPRIO) && AQ_SETPRIO == 4
+    asm volatile("s_setprio 0" ::: "memory");   // (k_stream priority experiment: the table reads are out)
+#endif
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         kd[k] = kd[k] - kk.shift;

@@ -182,6 +182,15 @@ constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without 
 #ifndef AQ_PRO_OVERLAP
 #define AQ_PRO_OVERLAP 1   // the prologue's exp-table loads overlap the rings' set-up (k_stream)
 #endif
+// Wave priority experiments (s_setprio, r03): 1 = a round's start (pop, midpoints, table reads)
+// at priority 3, from the end of its F chains on 0; 2 = a round's end (ballots, pushes, loop
+// control) at 2; 3 = only the pop at 3; 4 = 3 until the exp-table reads are issued (aq_libm.h hook);
+// 5 = as 1 at priority 2; 6 = as 1, dropping to 1
+// 7 = 3 from the pop to the end of the pushes; 8 = the whole burst at 3 (its outer loop at 0).
+// r03 A/B (profiles/r03s, r03t): 1, 5, 6 -0.8 %; 3 -0.1 %; 4 +1.0 %; 2 +2.6 %.
+#ifndef AQ_SETPRIO
+#define AQ_SETPRIO 1
+#endif
 #ifndef AQ_ONE_WINDOW
 #define AQ_ONE_WINDOW 0   // r03 A/B (profiles/r03q/ab.txt): 2 SALU fewer per round, 0.6 % SLOWER -- off
 #endif
@@ -1553,7 +1562,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
                 double pa, pb, pfa, pfm, pfb;
                 unsigned long long dtw;   // the pair word's 8-byte field (dt in its low half)
+                if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 3 || AQ_SETPRIO == 4 || AQ_SETPRIO == 6 ||
+                              AQ_SETPRIO == 7)
+                    asm volatile("s_setprio 3");
+                if constexpr (AQ_SETPRIO == 5) asm volatile("s_setprio 2");
+                if constexpr (AQ_SETPRIO == 2) asm volatile("s_setprio 0");
                 lds_pop6w(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dtw);
+                if constexpr (AQ_SETPRIO == 3) asm volatile("s_setprio 0");
                 const unsigned dt = (unsigned)dtw;
                 Step2 st[2];
                 // both midpoints lie in [pa, pb]: one range test for the pair
@@ -1571,6 +1586,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
                 double pm, hm;
                 pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+                if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 5) asm volatile("s_setprio 0");
+                if constexpr (AQ_SETPRIO == 6) asm volatile("s_setprio 1");
+                if constexpr (AQ_SETPRIO == 2) asm volatile("s_setprio 2");
                 // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
                 // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
                 // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
@@ -1634,6 +1652,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                 }
                 b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
+                if constexpr (AQ_SETPRIO == 7) asm volatile("s_setprio 0");
                 if constexpr (DIAG) {
                     if (lane == 0) {
                         const unsigned long long c2 = clk();
@@ -1648,6 +1667,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
                 }
         };
+        if constexpr (AQ_SETPRIO == 8) asm volatile("s_setprio 3");
         bool b_go;
         for (;;) {   // the burst: runs of rounds (the inner loops, their exits one compare each), and the
                      // cellar moves at the window's edges between them
@@ -1722,6 +1742,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             __builtin_amdgcn_wave_barrier();
             if (!b_go) break;
         }
+        if constexpr (AQ_SETPRIO == 8) asm volatile("s_setprio 0");
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;

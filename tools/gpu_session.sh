@@ -27,6 +27,7 @@ for step in "$@"; do
     diag)    run diag_1e10 120 python tools/diag_single.py --eps 1e-10 && run diag_1task 120 python tools/diag_single.py --eps 1e30 ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     xcd)     run xcd_start 120 python tools/xcd_start.py ;;
+    ulevel)  run ubench_level 120 tools/ubench_level ;;
     prof)    run prof 1000 bash tools/profile_round.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
