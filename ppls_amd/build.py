@@ -80,7 +80,14 @@ def build(force=False, verbose=False):
 if __name__ == "__main__":
     if "--variant" in sys.argv:   # python ppls_amd/build.py --variant NAME [-DX=1 ...]
         i = sys.argv.index("--variant")
-        print("built", build_variant(sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")]))
+        # -D... defines, and --mllvm=<option> for LLVM options (scheduler experiments)
+        extra = []
+        for a in sys.argv[i + 2:]:
+            if a.startswith("-D"):
+                extra.append(a)
+            elif a.startswith("--mllvm="):
+                extra += ["-mllvm", a[len("--mllvm="):]]
+        print("built", build_variant(sys.argv[i + 1], extra))
     else:
         build(force="--force" in sys.argv, verbose=True)
         print("built", LIB)

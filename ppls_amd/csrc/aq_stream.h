@@ -186,7 +186,8 @@ constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without 
 // at priority 3, from the end of its F chains on 0; 2 = a round's end (ballots, pushes, loop
 // control) at 2; 3 = only the pop at 3; 4 = 3 until the exp-table reads are issued (aq_libm.h hook);
 // 5 = as 1 at priority 2; 6 = as 1, dropping to 1
-// 7 = 3 from the pop to the end of the pushes; 8 = the whole burst at 3 (its outer loop at 0).
+// 7 = 3 from the pop to the end of the pushes; 8 = the whole burst at 3 (its outer loop at 0);
+// 9 = a fixed priority per wave (wave index mod 3).
 // r03 A/B (profiles/r03s, r03t): 1, 5, 6 -0.8 %; 3 -0.1 %; 4 +1.0 %; 2 +2.6 %.
 #ifndef AQ_SETPRIO
 #define AQ_SETPRIO 1
@@ -891,6 +892,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
     };
     const ExpConsts kk = pinned_exp_consts();
+    // AQ_SETPRIO 9: a fixed priority per wave (0 / 1 / 2 by wave index mod 3: one wave per SIMD runs
+    // ahead of its two siblings)
+    if constexpr (AQ_SETPRIO == 9) {
+        const unsigned pr = wid % 3u;
+        if (pr == 1u) asm volatile("s_setprio 1");
+        else if (pr == 2u) asm volatile("s_setprio 2");
+    }
     // the depth cap per burst (AQ_BURST_CAP); the histogram instance keeps the per-round test
     constexpr bool burst_cap = AQ_BURST_CAP != 0 && !HIST;
     // the round's accumulations and pushes in one exec window (not in the histogram / diagnostic

@@ -28,6 +28,7 @@ for step in "$@"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     xcd)     run xcd_start 120 python tools/xcd_start.py ;;
     ulevel)  run ubench_level 120 tools/ubench_level ;;
+    pmc)     run pmc 500 bash tools/pmc_profile.sh "pmc_$TAG" ;;
     prof)    run prof 1000 bash tools/profile_round.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -51,6 +51,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="_ZN2aq8k_streamILi0ELb0ELb0ELb0EEEvNS_12StreamParamsE")
     ap.add_argument("-D", action="append", default=[])
+    ap.add_argument("--mllvm", action="append", default=[], help="an LLVM option (e.g. -amdgpu-sched-strategy=max-ilp)")
     ap.add_argument("--dump", action="store_true", help="print the loop body")
     ap.add_argument("--first-backedge", action="store_true",
                     help="bottom-tested loop: count up to the first conditional back-edge")
@@ -58,7 +59,7 @@ def main():
     a = ap.parse_args()
     d = tempfile.mkdtemp()
     out = os.path.join(d, "k.s")
-    remarks = compile_asm(["-D" + x for x in a.D], out)
+    remarks = compile_asm(["-D" + x for x in a.D] + [y for m in a.mllvm for y in ("-mllvm", m)], out)
     s = open(out).read()
     i = s.index(a.kernel + ":")
     j = s.index(".Lfunc_end", i)

@@ -114,6 +114,18 @@ __global__ __launch_bounds__(256) void k_copy(const Rec* __restrict__ in, unsign
     }
 }
 
+// write-only and read-only passes of the same sizes
+__global__ __launch_bounds__(256) void k_write(Rec* __restrict__ out, unsigned n_out) {
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n_out) out[i] = Rec{(double)i, 1.0, 2.0, 3.0};
+}
+__global__ __launch_bounds__(256) void k_read(const Rec* __restrict__ in, unsigned n_in, double* sink) {
+    const unsigned i = blockIdx.x * 256 + threadIdx.x;
+    double v = 0.0;
+    if (i < n_in) { const Rec r = in[i]; v = r.l + r.r + r.fl + r.fr; }
+    if (v == 12345.678) sink[0] = v;   // never true for these records: keeps the loads
+}
+
 int main() {
     const unsigned n = 1652276;
     std::vector<Rec> h(n);
@@ -175,5 +187,30 @@ int main() {
     if (timeit("nostore", [&] { hipLaunchKernelGGL((k_lvl<true, false>), dim3(grid), dim3(T), 0, 0, din, n, dout, dn, eps, dparts, dtab); })) return 1;
     if (timeit("neither", [&] { hipLaunchKernelGGL((k_lvl<false, false>), dim3(grid), dim3(T), 0, 0, din, n, dout, dn, eps, dparts, dtab); })) return 1;
     if (timeit("copy", [&] { hipLaunchKernelGGL(k_copy, dim3((n + 255) / 256), dim3(256), 0, 0, din, n, dout, refined_children); })) return 1;
+    // (alg_GBps below counts the copy's bytes; the pure passes move only their own)
+    {
+        std::vector<float> t;
+        for (int rep = 0; rep < 12; ++rep) {
+            CHECK(hipEventRecord(a));
+            hipLaunchKernelGGL(k_write, dim3((refined_children + 255) / 256), dim3(256), 0, 0, dout, refined_children);
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms; CHECK(hipEventElapsedTime(&ms, a, b)); t.push_back(ms * 1e3f);
+        }
+        std::sort(t.begin(), t.end());
+        printf("{\"variant\": \"write_only\", \"bytes\": %.0f, \"us_median\": %.2f, \"GBps\": %.1f}\n",
+               32.0 * refined_children, t[6], 32.0 * refined_children / (t[6] * 1e-6) / 1e9);
+        t.clear();
+        for (int rep = 0; rep < 12; ++rep) {
+            CHECK(hipEventRecord(a));
+            hipLaunchKernelGGL(k_read, dim3((n + 255) / 256), dim3(256), 0, 0, din, n, dparts);
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms; CHECK(hipEventElapsedTime(&ms, a, b)); t.push_back(ms * 1e3f);
+        }
+        std::sort(t.begin(), t.end());
+        printf("{\"variant\": \"read_only\", \"bytes\": %.0f, \"us_median\": %.2f, \"GBps\": %.1f}\n",
+               32.0 * n, t[6], 32.0 * n / (t[6] * 1e-6) / 1e9);
+    }
     return 0;
 }
