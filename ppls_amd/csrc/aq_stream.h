@@ -130,6 +130,9 @@ constexpr int TAG_SHIFT = 16;
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
+#ifndef AQ_LONE_GSPLIT
+#define AQ_LONE_GSPLIT 1   // waves per share in launches of < 16 unsharded integrals (host side, aq_abi.inc)
+#endif
 #ifndef AQ_TASKS_PER_JOB
 #define AQ_TASKS_PER_JOB 40000   // A/B at 8192 integrals per launch: 8k 35.4, 15k 33.7, 25k 33.6, 40k 33.1, 60k 33.3, 100k 37.0 ms
 #endif

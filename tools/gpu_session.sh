@@ -29,6 +29,7 @@ for step in "$@"; do
     xcd)     run xcd_start 120 python tools/xcd_start.py ;;
     ulevel)  run ubench_level 120 tools/ubench_level ;;
     pmc)     run pmc 500 bash tools/pmc_profile.sh "pmc_$TAG" ;;
+    lonesplit) for g in 1 2 3 4; do AQ_GSPLIT=$g run lone_gsplit$g 120 python tools/try_single.py --reps 20; done ;;
     prof)    run prof 1000 bash tools/profile_round.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
