@@ -190,10 +190,14 @@ constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without 
 // control) at 2; 3 = only the pop at 3; 4 = 3 until the exp-table reads are issued (aq_libm.h hook);
 // 5 = as 1 at priority 2; 6 = as 1, dropping to 1
 // 7 = 3 from the pop to the end of the pushes; 8 = the whole burst at 3 (its outer loop at 0);
-// 9 = a fixed priority per wave (wave index mod 3).
+// 9 = a fixed priority per wave (wave index mod 3); 10 = as 1, stepping down to 2 once the exp-table
+// reads are written (no memory clobber: only a hint where they issue).
 // r03 A/B (profiles/r03s, r03t): 1, 5, 6 -0.8 %; 3 -0.1 %; 4 +1.0 %; 2 +2.6 %.
 #ifndef AQ_SETPRIO
 #define AQ_SETPRIO 1
+#endif
+#ifndef AQ_SEEDPRIO
+#define AQ_SEEDPRIO 0   // a job's seeding at priority 3 (the experiment beside AQ_SETPRIO)
 #endif
 #ifndef AQ_ONE_WINDOW
 #define AQ_ONE_WINDOW 0   // r03 A/B (profiles/r03q/ab.txt): 2 SALU fewer per round, 0.6 % SLOWER -- off
@@ -1045,6 +1049,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
             if (seed) {
                 // ---- wave-local seeding of job `job` (see the file header)
+                if constexpr (AQ_SEEDPRIO) asm volatile("s_setprio 3");
                 unsigned long long cs = 0;
                 if constexpr (DIAG) {
                     cs = clk();
@@ -1288,6 +1293,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         atomicMax(&s_dg[DG_T_SEEDED], rtc());
                     }
                 }
+                if constexpr (AQ_SEEDPRIO) asm volatile("s_setprio 0");
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
@@ -1574,7 +1580,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 double pa, pb, pfa, pfm, pfb;
                 unsigned long long dtw;   // the pair word's 8-byte field (dt in its low half)
                 if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 3 || AQ_SETPRIO == 4 || AQ_SETPRIO == 6 ||
-                              AQ_SETPRIO == 7)
+                              AQ_SETPRIO == 7 || AQ_SETPRIO == 10)
                     asm volatile("s_setprio 3");
                 if constexpr (AQ_SETPRIO == 5) asm volatile("s_setprio 2");
                 if constexpr (AQ_SETPRIO == 2) asm volatile("s_setprio 0");
@@ -1597,7 +1603,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
                 double pm, hm;
                 pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
-                if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 5) asm volatile("s_setprio 0");
+                if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 5 || AQ_SETPRIO == 10) asm volatile("s_setprio 0");
                 if constexpr (AQ_SETPRIO == 6) asm volatile("s_setprio 1");
                 if constexpr (AQ_SETPRIO == 2) asm volatile("s_setprio 2");
                 // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
