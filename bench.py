@@ -259,14 +259,18 @@ def main():
             return
         ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank, nshards=world)
 
-    # single-integral latency (one integral per launch), reported beside the throughput
+    # single-integral latency (one integral per launch), reported beside the throughput: on one GPU
+    # the kernel of the synchronous call a user makes for one integral (aq_integrate: its result slot
+    # is re-zeroed by the fetch, so nothing is enqueued before the launch), on N the rank's shard
     single_ms, single_n = 0.0, 0
     if not args.no_single:
-        launch(1)                     # untimed: the first K=1 launch pays the K=1 setup
+        from ppls_amd import Problem
+        one = (lambda: ctx.integrate(Problem(eps=args.eps))) if world == 1 else (lambda: launch(1))
+        one()                         # untimed: the first K=1 launch pays the K=1 setup
         ctx.synchronize()
         ctx.kernel_timing(True)
         for _ in range(max(args.warmup, 5)):
-            launch(1)
+            one()
         ctx.synchronize()
         single_ms, single_n = ctx.kernel_time()
         ctx.kernel_timing(False)

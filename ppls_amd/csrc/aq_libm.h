@@ -294,6 +294,9 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
 #if defined(AQ_SETPRIO) && AQ_SETPRIO == 4
     asm volatile("s_setprio 0" ::: "memory");   // (k_stream priority experiment: the table reads are out)
 #endif
+#if defined(AQ_SETPRIO) && AQ_SETPRIO == 10
+    asm volatile("s_setprio 2");                // (k_stream priority experiment: the chain's second half)
+#endif
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         kd[k] = kd[k] - kk.shift;

@@ -87,11 +87,16 @@ __host__ __device__ constexpr int seed_depth(unsigned long long V) {
 constexpr int GIVE_MIN = AQ_GIVE_MIN;        // a busy wave feeds the pool for idle siblings only above this size
 constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup donates from its pool
 #ifndef AQ_POLL_ROUNDS
-#define AQ_POLL_ROUNDS 64   // A/B r01q (8192 integrals, eps 1e-10): 16 34.26, 32 33.35, 64 32.95 ms per launch
+// A/B r01q (8192 integrals, eps 1e-10): 16 34.26, 32 33.35, 64 32.95 ms per launch; r03 (in-burst
+// moves, wave priority; the bench's 32768-integral launch, profiles/r03x): 128 with GIVE 64
+#define AQ_POLL_ROUNDS 64
 #endif
 constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
 #ifndef AQ_GIVE_ROUNDS
-#define AQ_GIVE_ROUNDS 32   // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged
+// r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged.
+// r03 (bursts no longer end at cellar moves, so the give / poll round is their main end): 64 / 128 with
+// 60 k-task jobs -1.8 % on the bench launch (profiles/r03x), 16 +1.5 %, 128 / 256 -0.5 %
+#define AQ_GIVE_ROUNDS 32
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 #ifndef AQ_SKEWED_GIVE
@@ -99,7 +104,7 @@ constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle sibli
 #endif
 constexpr int SKEWED_GIVE = AQ_SKEWED_GIVE;   // give rounds for the skewed built-in integrand (sin(1/x))
 #ifndef AQ_SKEWED_POLL
-#define AQ_SKEWED_POLL AQ_POLL_ROUNDS
+#define AQ_SKEWED_POLL 64   // (the measured sin(1/x) setting, kept when cosh4's poll went to 128)
 #endif
 constexpr int SKEWED_POLL = AQ_SKEWED_POLL;
 #ifndef AQ_SKEWED_GIVE_MIN
@@ -130,11 +135,22 @@ constexpr int TAG_SHIFT = 16;
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
+#ifndef AQ_LONE_GIVE
+#define AQ_LONE_GIVE 0       // give rounds of the per-CU instance (0: as the rest)
+#endif
+#ifndef AQ_LONE_POLL
+#define AQ_LONE_POLL 64
+#endif
+#ifndef AQ_LONE_GIVE_MIN
+#define AQ_LONE_GIVE_MIN 32
+#endif
 #ifndef AQ_LONE_GSPLIT
 #define AQ_LONE_GSPLIT 1   // waves per share in launches of < 16 unsharded integrals (host side, aq_abi.inc)
 #endif
 #ifndef AQ_TASKS_PER_JOB
-#define AQ_TASKS_PER_JOB 40000   // A/B at 8192 integrals per launch: 8k 35.4, 15k 33.7, 25k 33.6, 40k 33.1, 60k 33.3, 100k 37.0 ms
+// A/B at 8192 integrals per launch (r01): 8k 35.4, 15k 33.7, 25k 33.6, 40k 33.1, 60k 33.3, 100k 37.0 ms;
+// r03 at the bench's 32768 per launch (profiles/r03x): 60 k -1.8 % with give / poll 64 / 128, 80 k -1.3 %
+#define AQ_TASKS_PER_JOB 40000
 #endif
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
@@ -475,6 +491,11 @@ struct Acc {
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
     unsigned maxdt;                 // per lane: the deepest pair depth (dt's low byte) a round popped, or
                                     // with the per-burst cap (AQ_BURST_CAP) the deepest pair a round pushed
+    double r = 0.0;                 // per lane: the rounds' accepted areas of the current burst, a plain
+                                    // double (one masked add per accepted task), folded into hi / lo
+                                    // exactly at every burst's end -- so a lane's rounding error is that of
+                                    // a burst's few leaves, not of a whole job's (r03: 60 k-task jobs had
+                                    // let two schedules of one batch differ by > 2 ulp)
 };
 
 // Flush a wave's accumulators for integral `tag` and reset them: the wave's double-double area (hi
@@ -487,6 +508,9 @@ struct Acc {
 template <int FID, bool PCU>
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, WgState& S,
                                           unsigned long long* pc, XSum* px) {
+    // (the rounds' lane partial is folded at every burst's end; fold any remainder here too)
+    dd_add(a.hi, a.lo, a.r);
+    a.r = 0.0;
     // a wave that ran no task of `tag` has nothing to add (idle waves at the exit of a lone launch)
     if (uni(a.ut) != 0u || __ballot(a.tasks != 0u) != 0ull) {
         // the wave accumulates doubled areas for the built-in integrands (exact halving, aq_device.h)
@@ -871,9 +895,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // sin(1/x) (config 4) piles nearly all of its tree into one small region: its waves look for idle
     // siblings every SKEWED_GIVE rounds (a lone integral 79 -> 70 us at 4; cosh4 keeps 32, where 4 cost
     // the eps=1e-12 lone tree 47 -> 61 us and the bench 0.6 %; profiles/r02_ab/fast_give_poll*.txt)
-    constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE : (unsigned)GIVE_ROUNDS;
-    constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL : (unsigned)POLL_ROUNDS;
-    constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN : (unsigned)GIVE_MIN;
+    // (the per-CU instance -- launches of a few integrals -- may use its own cadence, AQ_LONE_GIVE*)
+    constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE
+                                     : (PCU && AQ_LONE_GIVE > 0) ? (unsigned)AQ_LONE_GIVE : (unsigned)GIVE_ROUNDS;
+    constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL
+                                     : (PCU && AQ_LONE_GIVE > 0) ? (unsigned)AQ_LONE_POLL : (unsigned)POLL_ROUNDS;
+    constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN
+                                  : (PCU && AQ_LONE_GIVE > 0) ? (unsigned)AQ_LONE_GIVE_MIN : (unsigned)GIVE_MIN;
     unsigned poll_ctr = wid * (poll_rounds / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
@@ -1631,7 +1659,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned long long cdtw = dtw + 1ull;         // depth + 1, same integral
                 const unsigned cdt = (unsigned)cdtw;
                 if constexpr (!one_window)
-                    masked_acc3(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                    masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
                                 burst_cap ? (mask0 | mask1) : am);
                 if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
                                         // takes and seeds switch the tag); checked in diagnostic builds
@@ -1651,7 +1679,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
                 const unsigned cnt0 = (unsigned)__popcll(mask0);
                 if constexpr (one_window) {
-                    acc3_push6x2<FULL>(acc.hi, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                    acc3_push6x2<FULL>(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
                                  burst_cap ? (mask0 | mask1) : am,
                                  mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
                                  mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
@@ -1771,6 +1799,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // tasks as well: those count as accepted here, and the launch reports ERRB_DEPTH)
         acc.ut += 2u * b_n;
         acc.ul += b_n - (b_top - b_top0);
+        dd_add(acc.hi, acc.lo, acc.r);   // the burst's lane partial, exactly into the double-double
+        acc.r = 0.0;
         if (b_dv) err |= ERRB_DEPTH;
         if constexpr (burst_cap) {
             // the per-burst depth cap: a pushed pair at depth >= max_depth means a task at the cap

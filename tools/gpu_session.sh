@@ -29,6 +29,12 @@ for step in "$@"; do
     xcd)     run xcd_start 120 python tools/xcd_start.py ;;
     ulevel)  run ubench_level 120 tools/ubench_level ;;
     pmc)     run pmc 500 bash tools/pmc_profile.sh "pmc_$TAG" ;;
+    tests_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run gpu_tests_tuned 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    bench_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run bench_tuned 400 python bench.py ;;
+    bench12_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run bench12_tuned 400 python bench.py --eps 1e-12 --batch 4096 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    prof_t)  AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run prof_tuned 1000 bash tools/profile_round.sh "${TAG}t" ;;
+    diagk)   run diag_k32768 300 python tools/diag_persist.py --k 32768 --reps 2 ;;
+    lonevar) for so in ppls_amd/_build/${AB_GLOB_L:-libaquad_*.so}; do n=$(basename $so .so); AQ_LIB=$PWD/$so run lone_$n 120 python tools/try_single.py --reps 20; done ;;
     lonesplit) for g in 1 2 3 4; do AQ_GSPLIT=$g run lone_gsplit$g 120 python tools/try_single.py --reps 20; done ;;
     prof)    run prof 1000 bash tools/profile_round.sh "$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
