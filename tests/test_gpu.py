@@ -645,3 +645,34 @@ def test_rccl_group_join(ctx, trees):
         r = grp.integrate(Problem(eps=1e-10, n_gpus=1))
     g = trees["cosh4_eps1e-10"]
     assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hist", [False, True])
+def test_depth_cap_boundary(ctx, trees, hist):
+    """The depth cap (max_depth) at its exact boundary. The bench instance checks it once per burst
+    (AQ_BURST_CAP: the deepest pushed pair against max_depth at the burst's end), the histogram
+    instance per round; both must agree with the reference's refinement to the level: cosh4 at
+    eps=1e-10 has levels L = 23 (its deepest tasks at depth 22), so max_depth = L runs exactly and
+    max_depth = L - 1 fails with AQ_EDEPTH -- for a lone launch (per-CU instance) and a 64-integral
+    launch; the context stays usable."""
+    from ppls_amd import AquadError, Problem
+    g = trees["cosh4_eps1e-10"]
+    L = g["levels"]
+    ctx.set_level_histograms(hist)
+    try:
+        r = ctx.integrate(Problem(eps=1e-10, max_depth=L))
+        assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], L)
+        with pytest.raises(AquadError, match="depth"):
+            ctx.integrate(Problem(eps=1e-10, max_depth=L - 1))
+        k = 64
+        ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-10, first_slot=0, max_depth=L)
+        for i in range(k):
+            r = ctx.fetch(i)
+            assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], L)
+        ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-10, first_slot=0, max_depth=L - 1)
+        with pytest.raises(AquadError, match="depth"):
+            ctx.fetch(0)
+    finally:
+        ctx.set_level_histograms(True)   # the context's default
+    assert ctx.integrate(Problem(eps=1e-3)).tasks == 6567
