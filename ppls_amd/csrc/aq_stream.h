@@ -89,14 +89,14 @@ constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup dona
 #ifndef AQ_POLL_ROUNDS
 // A/B r01q (8192 integrals, eps 1e-10): 16 34.26, 32 33.35, 64 32.95 ms per launch; r03 (in-burst
 // moves, wave priority; the bench's 32768-integral launch, profiles/r03x): 128 with GIVE 64
-#define AQ_POLL_ROUNDS 64
+#define AQ_POLL_ROUNDS 128
 #endif
 constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
 #ifndef AQ_GIVE_ROUNDS
 // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged.
 // r03 (bursts no longer end at cellar moves, so the give / poll round is their main end): 64 / 128 with
 // 60 k-task jobs -1.8 % on the bench launch (profiles/r03x), 16 +1.5 %, 128 / 256 -0.5 %
-#define AQ_GIVE_ROUNDS 32
+#define AQ_GIVE_ROUNDS 64
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 #ifndef AQ_SKEWED_GIVE
@@ -150,7 +150,7 @@ constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's 
 #ifndef AQ_TASKS_PER_JOB
 // A/B at 8192 integrals per launch (r01): 8k 35.4, 15k 33.7, 25k 33.6, 40k 33.1, 60k 33.3, 100k 37.0 ms;
 // r03 at the bench's 32768 per launch (profiles/r03x): 60 k -1.8 % with give / poll 64 / 128, 80 k -1.3 %
-#define AQ_TASKS_PER_JOB 40000
+#define AQ_TASKS_PER_JOB 60000
 #endif
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
