@@ -135,6 +135,9 @@ constexpr int TAG_SHIFT = 16;
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
+#ifndef AQ_EARLY_FLUSH
+#define AQ_EARLY_FLUSH 0
+#endif
 #ifndef AQ_LONE_GIVE
 #define AQ_LONE_GIVE 0       // give rounds of the per-CU instance (0: as the rest)
 #endif
@@ -1013,6 +1016,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (fresh && job < total_jobs) {
                 seed = true;
             } else {
+                // per-CU launches (a few integrals): a wave with nothing left to seed flushes its
+                // accumulators before it looks for pool work or goes idle -- while other waves still
+                // run, instead of every wave flushing at once after the run's end (AQ_EARLY_FLUSH)
+                if constexpr (PCU && AQ_EARLY_FLUSH)
+                    if (!counted_idle && job >= total_jobs) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
                 wave_lock(&S.lock, lane, lock_spins);
                 {
                     const unsigned avail = uni(S.ptop - S.pbot);
