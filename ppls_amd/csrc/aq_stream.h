@@ -135,6 +135,9 @@ constexpr int TAG_SHIFT = 16;
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
+#ifndef AQ_LONE_BLOCK
+#define AQ_LONE_BLOCK 0   // lone launches: contiguous blocks of 2^s seed positions per share (0: snake)
+#endif
 #ifndef AQ_EARLY_FLUSH
 #define AQ_EARLY_FLUSH 0
 #endif
@@ -409,6 +412,8 @@ struct StreamParams {
     double2 kbounds[PCU_MAXK];      // per-CU launches: the bounds again, as kernel arguments (a scalar load
                                     // with the launch's other arguments, not a cold HBM line at seeding)
     int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
+    int block_s;                    // > 0: share sh seeds the 2^block_s contiguous positions [sh << s, ..)
+                                    // (lone launches, AQ_LONE_BLOCK); 0: the snake partition
 };
 
 // Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
@@ -1157,7 +1162,81 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 unsigned long long cp1 = 0, cp2 = 0;
                 bool alive = false;
                 double l = A, r = B, fl = 0.0, fr = 0.0, mid = 0.0, fmid = 0.0;
-                if (nnodes <= 64) {
+                if (P.block_s > 0) {
+                    // contiguous blocks (lone launches, AQ_LONE_BLOCK): share sh owns the 2^s positions
+                    // [sh << s, (sh + 1) << s) at depth D = Dp + s, so its nodes are the path of its block
+                    // root (depths 0..Dp-1: lane d) and the block's whole subtree (depth Dp + e, index
+                    // t < 2^e: lane Dp + 2^e - 1 + t) -- each surviving wave starts with up to 2^s pairs
+                    // where the snake deal's 3 positions gave it ~3 (a lone tree's rounds were half
+                    // empty for their first five). A path node is owned by the share whose block starts
+                    // at its leftmost position, a subtree node by its block's share: every node at depth
+                    // <= D is counted once, as in the snake partition.
+                    const unsigned sb = (unsigned)P.block_s;
+                    const unsigned Dp = (unsigned)D - sb;
+                    const unsigned nn = Dp + (2u << sb) - 1u;   // + F(A), F(B): <= 64 (host-checked)
+                    const unsigned q = lane;
+                    const bool isnode = q < nn;
+                    unsigned d = 0;
+                    unsigned long long g = 0;   // the node's index at its depth
+                    if (isnode) {
+                        if (q < Dp) {
+                            d = q;
+                            g = (unsigned long long)sh >> (Dp - d);
+                        } else {
+                            const unsigned u = q - Dp, e = 31u - (unsigned)__builtin_clz(u + 1u);
+                            d = Dp + e;
+                            g = ((unsigned long long)sh << e) + (u - ((1u << e) - 1u));
+                        }
+                    }
+                    // the lane of this node's ancestor at depth i < d
+                    auto lane_of = [&](unsigned i) -> unsigned {
+                        const unsigned long long gi = g >> (d - i);
+                        if (i < Dp) return i;
+                        const unsigned e = i - Dp;
+                        return Dp + ((1u << e) - 1u) + (unsigned)(gi - ((unsigned long long)sh << e));
+                    };
+                    unsigned li = nn, ri = nn + 1u;
+                    unsigned long long ancm = 0;   // the ancestors' lanes
+                    for (unsigned i = 0; i < d; ++i) {
+                        const double mm = (l + r) / 2;
+                        const unsigned la = lane_of(i);
+                        ancm |= 1ull << la;
+                        if ((g >> (d - 1u - i)) & 1ull) { l = mm; li = la; } else { r = mm; ri = la; }
+                    }
+                    mid = (l + r) / 2;                                        // :187
+                    if (q < nn + 2u) {
+                        fmid = integrand<FID>(isnode ? mid : (q == nn ? A : B), tab);   // :188
+                        fm[q] = fmid;
+                    }
+                    bool refine = false;
+                    double leafarea = 0.0;
+                    if (isnode) {
+                        fl = fm[li];
+                        fr = fm[ri];
+                        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
+                        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
+                        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
+                        refine = fabs((larea + rarea) - lrarea) > eps;       // :191
+                        leafarea = larea + rarea;                             // :199
+                    }
+                    const unsigned long long leafm = __ballot(isnode && !refine);
+                    const bool reach = isnode && (leafm & ancm) == 0ull;     // no leaf above it: it exists
+                    const bool owned = d >= Dp || (sh & ((1u << (Dp - d)) - 1u)) == 0u;
+                    if (reach && owned) {
+                        ++acc.tasks;
+                        acc.maxd = max(acc.maxd, d + 1u);
+                        if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
+                        if (!refine) {
+                            dd_add(acc.hi, acc.lo, leafarea / area_scale<FID>());   // :199 -> :149 (doubled, exact)
+                            ++acc.leaves;
+                            if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
+                        } else if ((int)d + 1 >= max_depth) {
+                            err |= ERRB_DEPTH;
+                        }
+                    }
+                    alive = reach && refine && d == (unsigned)D && D + 1 < max_depth;
+                    if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
+                } else if (nnodes <= 64) {
                     // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
                     // decision; the first leaf depth of every position comes from ONE ballot
                     unsigned long long ca = 0, cb = 0;

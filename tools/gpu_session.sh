@@ -30,6 +30,7 @@ for step in "$@"; do
     ulevel)  run ubench_level 120 tools/ubench_level ;;
     pmc)     run pmc 500 bash tools/pmc_profile.sh "pmc_$TAG" ;;
     tests_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run gpu_tests_tuned 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    tests_v) AQ_LIB=$PWD/ppls_amd/_build/${TEST_LIB:?} run gpu_tests_${TEST_LIB%.so} 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     bench_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run bench_tuned 400 python bench.py ;;
     bench12_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run bench12_tuned 400 python bench.py --eps 1e-12 --batch 4096 --steps 4 --warmup 1 --no-cpu-baseline ;;
     prof_t)  AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run prof_tuned 1000 bash tools/profile_round.sh "${TAG}t" ;;
