@@ -45,7 +45,7 @@ extern "C" {
 /* Integrand = the reference's F(arg) macro (aquadPartA.c:46) as a compile-time kernel variant. */
 typedef enum {
     AQ_F_COSH4 = 0,     /* cosh(x)*cosh(x)*cosh(x)*cosh(x), glibc-2.35-exact cosh (the reference), |x| <= 170 */
-    AQ_F_SIN_RECIP = 1, /* sin(1/x) (SURVEY config 4) */
+    AQ_F_SIN_RECIP = 1, /* sin(1/x) (SURVEY config 4), glibc-exact for |x| > 9.5e-9 */
     AQ_F_USER = 2       /* the plug-in compiled in from AQ_USER_F_HEADER (aq_user_integrand_name()) */
 } aq_integrand;
 

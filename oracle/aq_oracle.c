@@ -15,6 +15,8 @@
  *   - __ieee754_cosh   (sysdeps/ieee754/dbl-64/e_cosh.c, fdlibm formula)
  *   - __exp            (sysdeps/ieee754/dbl-64/e_exp.c, N=128 table; FMA and non-FMA ifunc forms)
  *   - __expm1          (sysdeps/ieee754/dbl-64/s_expm1.c, k=0 path, Estrin polynomial)
+ *   - __sin            (sysdeps/ieee754/dbl-64/s_sin.c, |x| < 105414350; FMA and non-FMA forms) for
+ *                      the config-4 F macro sin(1.0/(arg))
  * Pinning: tests/test_oracle.py checks these bit for bit against the host libm and the
  * whole tree walk against the reference's header known answer (aquadPartA.c:31-36) and
  * against fixtures produced by the compiled reference (oracle/Makefile -> oracle/_ref/).
@@ -169,15 +171,100 @@ double aqo_cosh(double x, int fma_variant)
     return INFINITY;
 }
 
+/* ---- glibc 2.35 __sin (s_sin.c, IBM Accurate Mathematical Library), |x| < 105414350 -------
+ * The config-4 F macro is sin(1.0/(arg)). Both ifunc forms: the FMA one (__sin_fma, what x86_64
+ * hosts with FMA select) is GCC's contraction of the same source -- every a*b+c of the Taylor and
+ * table-correction polynomials, of the cor sums and of the Cody-Waite reduction fuses, and of the
+ * two-product sums it fuses the left product (p*a - 0.5*da, x*dx + xx*(...)); MAC below spells that
+ * out (this file builds with -ffp-contract=off). tests/test_oracle.py pins the FMA form to the host
+ * libm. Beyond 105414350 glibc reduces with __branred (Payne-Hanek), not restated here: the host
+ * sin answers there. */
+#include "glibc_sincos_table.h"
+static const double Ss1 = -0x1.5555555555555p-3, Ss2 = 0.0083333333333323288, Ss3 = -1.9841269834414642e-04,
+                    Ss4 = 2.755729806860771e-06, Ss5 = -2.5022014848318398e-08;
+static const double Sn3 = -1.66666666666664880952546298448555E-01, Sn5 = 8.33333214285722277379541354343671E-03,
+                    Cs2 = 4.99999999999999999999950396842453E-01, Cs4 = -4.16666666666664434524222570944589E-02,
+                    Cs6 = 1.38888874007937613028114285595617E-03;
+static const double SBig = 0x1.8p45, SHp0 = 0x1.921FB54442D18p0, SHp1 = 0x1.1A62633145C07p-54,
+                    SMp1 = 0x1.921FB58p0, SMp2 = -0x1.DDE973Cp-27, SPp3 = -0x1.CB3B398p-55,
+                    SPp4 = -0x1.d747f23e32ed7p-83, SHpinv = 0x1.45F306DC9C883p-1, SToint = 0x1.8p52;
+#define MAC(fv, a, b, c) ((fv) ? fma((a), (b), (c)) : (a) * (b) + (c))
+
+static double aqo_sin_do_cos(double x, double dx, int fv)
+{
+    if (x < 0) dx = -dx;
+    double u = SBig + fabs(x);
+    x = fabs(x) - (u - SBig) + dx;
+    double xx = x * x;
+    double s = MAC(fv, x * xx, MAC(fv, xx, Sn5, Sn3), x);
+    double c = xx * MAC(fv, xx, MAC(fv, xx, Cs6, Cs4), Cs2);
+    int k = (int)(uint32_t)asu(u) << 2;
+    double sn = aqo_sincos_tab[k], ssn = aqo_sincos_tab[k + 1], cs = aqo_sincos_tab[k + 2], ccs = aqo_sincos_tab[k + 3];
+    double cor = MAC(fv, -sn, s, MAC(fv, -cs, c, MAC(fv, -s, ssn, ccs)));
+    return cs + cor;
+}
+
+static double aqo_sin_do_sin(double x, double dx, int fv)
+{
+    double xold = x;
+    if (fabs(x) < 0.126) {          /* TAYLOR_SIN (x*x, x, dx) */
+        double xx = x * x;
+        double p = MAC(fv, MAC(fv, MAC(fv, MAC(fv, Ss5, xx, Ss4), xx, Ss3), xx, Ss2), xx, Ss1);
+        double t = MAC(fv, MAC(fv, p, x, -0.5 * dx), xx, dx);
+        return x + t;
+    }
+    if (x <= 0) dx = -dx;
+    double u = SBig + fabs(x);
+    x = fabs(x) - (u - SBig);
+    double xx = x * x;
+    double s = x + MAC(fv, x * xx, MAC(fv, xx, Sn5, Sn3), dx);
+    double c = MAC(fv, x, dx, xx * MAC(fv, xx, MAC(fv, xx, Cs6, Cs4), Cs2));
+    int k = (int)(uint32_t)asu(u) << 2;
+    double sn = aqo_sincos_tab[k], ssn = aqo_sincos_tab[k + 1], cs = aqo_sincos_tab[k + 2], ccs = aqo_sincos_tab[k + 3];
+    double cor = MAC(fv, cs, s, MAC(fv, -sn, c, MAC(fv, s, ccs, ssn)));
+    return copysign(sn + cor, xold);
+}
+
+double aqo_sin(double x, int fma_variant)
+{
+    uint32_t k = (uint32_t)(asu(x) >> 32) & 0x7fffffff;
+    if (k < 0x3e500000) return x;                                   /* |x| < 2^-26 */
+    if (k < 0x3feb6000) return aqo_sin_do_sin(x, 0.0, fma_variant);  /* |x| < 0.855469 */
+    if (k < 0x400368fd) {                                           /* |x| < 2.426265 */
+        double t = SHp0 - fabs(x);
+        return copysign(aqo_sin_do_cos(t, SHp1, fma_variant), x);
+    }
+    if (k < 0x419921FB) {                                           /* |x| < 105414350 */
+        double t = MAC(fma_variant, x, SHpinv, SToint);
+        double xn = t - SToint;
+        double y = MAC(fma_variant, -xn, SMp2, MAC(fma_variant, -xn, SMp1, x));
+        int n = (int)((uint32_t)asu(t) & 3);
+        double t1 = xn * SPp3, t2 = y - t1, db = (y - t2) - t1;
+        t1 = xn * SPp4;
+        double b = t2 - t1;
+        db += (t2 - b) - t1;
+        double r = (n & 1) ? aqo_sin_do_cos(b, db, fma_variant) : aqo_sin_do_sin(b, db, fma_variant);
+        return (n & 2) ? -r : r;
+    }
+    return sin(x);                                                  /* __branred range, inf, nan */
+}
+#undef MAC
+
 /* libm modes for F: restated glibc (FMA / non-FMA ifunc forms) or the host libm itself. */
 #define AQO_LIBM_RESTATED_FMA 0
 #define AQO_LIBM_RESTATED_NOFMA 1
 #define AQO_LIBM_HOST 2
 
+void aqo_sin_array(int mode, long n, const double *x, double *out)
+{
+    for (long i = 0; i < n; i++) out[i] = mode == AQO_LIBM_HOST ? sin(x[i]) : aqo_sin(x[i], mode == AQO_LIBM_RESTATED_FMA);
+}
+
 /* F(arg) exactly as the reference macro expands: cosh(a)*cosh(a)*cosh(a)*cosh(a), left to right. */
 static inline double F_eval(int integrand, int mode, double x)
 {
-    if (integrand == AQO_F_SIN_RECIP) return sin(1.0 / x);
+    if (integrand == AQO_F_SIN_RECIP)
+        return mode == AQO_LIBM_HOST ? sin(1.0 / x) : aqo_sin(1.0 / x, mode == AQO_LIBM_RESTATED_FMA);
     if (integrand == AQO_F_USER) {
         double y = -x * x;                  /* the macro expands to -(arg)*(arg) = (-x)*x */
         if (mode == AQO_LIBM_HOST) return exp(y);

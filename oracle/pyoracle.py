@@ -71,7 +71,7 @@ def lib():
         L.aqo_integrate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_int, ctypes.POINTER(_Res), up, up]
         L.aqo_integrate.restype = ctypes.c_int
-        for name in ("aqo_cosh_array", "aqo_exp_array", "aqo_expm1_array"):
+        for name in ("aqo_cosh_array", "aqo_exp_array", "aqo_expm1_array", "aqo_sin_array"):
             getattr(L, name).argtypes = [ctypes.c_int, ctypes.c_long, dp, dp]
             getattr(L, name).restype = None
         L.aqo_integrate_shard.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
@@ -151,6 +151,14 @@ def expm1(x, mode=RESTATED_FMA):
     x = np.ascontiguousarray(x, np.float64)
     out = np.empty_like(x)
     lib().aqo_expm1_array(mode, x.size, _dp(x), _dp(out))
+    return out
+
+
+def sin(x, mode=RESTATED_FMA):
+    """glibc 2.35 sin restated (aq_oracle.c aqo_sin), or the host libm's with HOST_LIBM."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    lib().aqo_sin_array(mode, x.size, _dp(x), _dp(out))
     return out
 
 

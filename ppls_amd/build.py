@@ -33,7 +33,7 @@ SOURCES = [os.path.join(CSRC, "aquad.hip")]
 # AQ_F_USER plug-in header (the reference's F(arg) macro, aquadPartA.c:46): the default Gaussian,
 # or any header named by PPLS_AMD_USER_F (see csrc/plugins/aq_user_gauss.h for the interface)
 USER_F = os.path.abspath(os.environ.get("PPLS_AMD_USER_F") or os.path.join(CSRC, "plugins", "aq_user_gauss.h"))
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_device.h", "aq_stream.h",
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_sincos_table.h", "aq_device.h", "aq_stream.h",
                                                   "aq_xsum.h", "aq_abi.inc")] + \
     [os.path.join(ROOT, "include", "aquad.h"), USER_F]
 LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
@@ -62,6 +62,8 @@ def build(force=False, verbose=False):
     tab = os.path.join(CSRC, "aq_exp_table.h")
     if not os.path.exists(tab):
         subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_exp_table.py")])
+    if not os.path.exists(os.path.join(CSRC, "aq_sincos_table.h")):
+        subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_sincos_table.py")])
     if force or _stale(LIB, DEPS):
         cmd = [HIPCC] + HIP_FLAGS + [f'-DAQ_USER_F_HEADER="{USER_F}"', "-o", LIB] + SOURCES + LIBS
         if verbose:

@@ -6,7 +6,9 @@
 // restates glibc's cosh exactly rather than calling OCML:
 //   __ieee754_cosh (e_cosh.c, fdlibm formula) over
 //   __exp          (e_exp.c, N=128 table, the FMA ifunc form x86_64 hosts with FMA select) and
-//   __expm1        (s_expm1.c, k = 0 path, Estrin polynomial, no fusion).
+//   __expm1        (s_expm1.c, k = 0 path, Estrin polynomial, no fusion),
+// and, for the config-4 variant of the macro, sin(1.0/(arg)):
+//   __sin          (s_sin.c, |x| < 105414350, the FMA ifunc form; table aq_sincos_table.h).
 // The kernels that include this header are compiled with -ffp-contract=off: every fusion below
 // is an explicit __fma_rn() placed exactly where GCC fused glibc's source.
 //
@@ -21,6 +23,8 @@
 #endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "aq_sincos_table.h"
 
 #pragma clang fp contract(off)
 
@@ -201,6 +205,84 @@ __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restric
     return __longlong_as_double(0x7ff0000000000000LL);
 }
 
+// glibc 2.35 sin (sysdeps/ieee754/dbl-64/s_sin.c), the config-4 F macro's sin(1.0/(arg)), as the
+// x86_64 __sin_fma ifunc variant evaluates it (the host libm the reference runs on): GCC's
+// contraction of the source fuses every a*b+c of the polynomials, the cor sums and the Cody-Waite
+// reduction, and the left product of p*a - 0.5*da and x*dx + xx*(...); the __fma_rn()s below spell that
+// out as __fma_rn (this file builds with -ffp-contract=off). The table {sin, cos} of i/128 as double-doubles
+// (aq_sincos_table.h) sits in constant memory: config 4 is one skewed tree, not the bench path.
+// Exact for |x| < 105414350 (|arg| > 9.5e-9); beyond that glibc's __branred (Payne-Hanek) is not
+// restated and the device libm's faithful sin answers.
+static __constant__ double kSinCosTab[AQ_SINCOS_TAB_N] = {AQ_SINCOS_TAB_INIT};
+
+namespace sinc {
+constexpr double s1 = -0x1.5555555555555p-3, s2 = 0.0083333333333323288, s3 = -1.9841269834414642e-04,
+                 s4 = 2.755729806860771e-06, s5 = -2.5022014848318398e-08;
+constexpr double sn3 = -1.66666666666664880952546298448555E-01, sn5 = 8.33333214285722277379541354343671E-03,
+                 cs2 = 4.99999999999999999999950396842453E-01, cs4 = -4.16666666666664434524222570944589E-02,
+                 cs6 = 1.38888874007937613028114285595617E-03;
+constexpr double big = 0x1.8p45, hp0 = 0x1.921FB54442D18p0, hp1 = 0x1.1A62633145C07p-54, mp1 = 0x1.921FB58p0,
+                 mp2 = -0x1.DDE973Cp-27, pp3 = -0x1.CB3B398p-55, pp4 = -0x1.d747f23e32ed7p-83,
+                 hpinv = 0x1.45F306DC9C883p-1, toint = 0x1.8p52;
+}  // namespace sinc
+
+__device__ __forceinline__ double sin_tab_cos(double x, double dx) {   // s_sin.c do_cos
+    using namespace sinc;
+    if (x < 0) dx = -dx;
+    const double u = big + fabs(x);
+    x = fabs(x) - (u - big) + dx;
+    const double xx = x * x;
+    const double s = __fma_rn(x * xx, __fma_rn(xx, sn5, sn3), x);
+    const double c = xx * __fma_rn(xx, __fma_rn(xx, cs6, cs4), cs2);
+    const int k = __double2loint(u) << 2;
+    const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+    const double cor = __fma_rn(-sn, s, __fma_rn(-cs, c, __fma_rn(-s, ssn, ccs)));
+    return cs + cor;
+}
+
+__device__ __forceinline__ double sin_tab_sin(double x, double dx) {   // s_sin.c do_sin
+    using namespace sinc;
+    const double xold = x;
+    if (fabs(x) < 0.126) {                                               // TAYLOR_SIN (x*x, x, dx)
+        const double xx = x * x;
+        const double p = __fma_rn(__fma_rn(__fma_rn(__fma_rn(s5, xx, s4), xx, s3), xx, s2), xx, s1);
+        return x + __fma_rn(__fma_rn(p, x, -0.5 * dx), xx, dx);
+    }
+    if (x <= 0) dx = -dx;
+    const double u = big + fabs(x);
+    x = fabs(x) - (u - big);
+    const double xx = x * x;
+    const double s = x + __fma_rn(x * xx, __fma_rn(xx, sn5, sn3), dx);
+    const double c = __fma_rn(x, dx, xx * __fma_rn(xx, __fma_rn(xx, cs6, cs4), cs2));
+    const int k = __double2loint(u) << 2;
+    const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+    const double cor = __fma_rn(cs, s, __fma_rn(-sn, c, __fma_rn(s, ccs, ssn)));
+    return copysign(sn + cor, xold);
+}
+
+__device__ __forceinline__ double sin_glibc(double x) {
+    using namespace sinc;
+    const unsigned k = (unsigned)__double2hiint(x) & 0x7fffffffu;
+    if (k < 0x3e500000u) return x;                                       // |x| < 2^-26
+    if (k < 0x3feb6000u) return sin_tab_sin(x, 0.0);                     // |x| < 0.855469
+    if (k < 0x400368fdu) return copysign(sin_tab_cos(hp0 - fabs(x), hp1), x);   // |x| < 2.426265
+    if (k < 0x419921fbu) {                                               // |x| < 105414350
+        const double t = __fma_rn(x, hpinv, toint);
+        const double xn = t - toint;
+        const double y = __fma_rn(-xn, mp2, __fma_rn(-xn, mp1, x));
+        const int n = __double2loint(t) & 3;
+        double t1 = xn * pp3;
+        const double t2 = y - t1;
+        double db = (y - t2) - t1;
+        t1 = xn * pp4;
+        const double b = t2 - t1;
+        db += (t2 - b) - t1;
+        const double r = (n & 1) ? sin_tab_cos(b, db) : sin_tab_sin(b, db);
+        return (n & 2) ? -r : r;
+    }
+    return sin(x);                                                       // __branred range, inf, nan
+}
+
 // Integrand ids (include/aquad.h aq_integrand).
 enum : int { F_COSH4 = 0, F_SIN_RECIP = 1, F_USER = 2 };
 
@@ -231,9 +313,7 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
     } else if constexpr (FID == F_USER) {
         return user::F(x, tab);
     } else {
-        // SURVEY config 4: sin(1/x). Leaf counts are insensitive to +-1 ulp in sin,
-        // so the device libm's faithful sin is used.
-        return sin(1.0 / x);
+        return sin_glibc(1.0 / x);   // SURVEY config 4: sin(1.0/(arg)) with glibc's sin
     }
 }
 
@@ -415,7 +495,7 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
         for (int k = 0; k < K; ++k) f[k] = user::F(x[k], tab);
     } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) f[k] = sin(1.0 / x[k]);
+        for (int k = 0; k < K; ++k) f[k] = sin_glibc(1.0 / x[k]);
     }
 }
 

@@ -40,6 +40,12 @@ def plugin_bits():
 
 
 @pytest.fixture(scope="session")
+def sin_bits():
+    z = np.load(os.path.join(GOLDEN, "sin_bits.npz"))  # allow_pickle=False (default)
+    return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
 def libm_bits():
     z = np.load(os.path.join(GOLDEN, "libm_bits.npz"))  # allow_pickle=False (default)
     return {k: z[k] for k in z.files}

@@ -17,6 +17,7 @@ Outputs (data only, no code of the reference):
   batch.json      splitmix64 batch bounds KATs and per-integral counts (config C3 prefix)
   plugin_bits.npz x, F(x) of the AQ_F_USER plug-in (exp(-x*x), host libm) as uint64 bit patterns
   deep.json       eps 1e-14 .. 1e-16 cosh4 trees pinned by the reference binary's task totals
+  sin_bits.npz    x, F(x) = sin(1.0/x) (config 4's F macro, host libm) as uint64 bit patterns
 """
 import json
 import os
@@ -204,6 +205,24 @@ def plugin():
     np.savez_compressed(os.path.join(OUT, "plugin_bits.npz"), x=x.view(np.uint64), F=F.view(np.uint64))
 
 
+def sin_bits():
+    """Config 4's F(arg) = sin(1.0/(arg)) from the host glibc 2.35 libm at points of its domain
+    [1e-4, 1], log-uniform points across every s_sin.c range of 1/x (|1/x| < 105414350), negative
+    points, and both sides of each range boundary of 1/x (0.855469, 2.426265, 105414350)."""
+    rng = np.random.default_rng(20261017)
+    edges = []
+    for e in (0.85546875, 2.4262657165527344, 105414350.0, 0.126, 1.0, 2.0 ** -26):
+        for v in (e, np.nextafter(e, 0.0), np.nextafter(e, 2 * e), e * (1 + 1e-9), e * (1 - 1e-9)):
+            edges += [1.0 / v, -1.0 / v]
+    x = np.concatenate([np.array(edges), rng.uniform(1e-4, 1.0, 8000),
+                        np.exp(rng.uniform(np.log(9.5e-9), np.log(10.0), 3000)),
+                        -rng.uniform(1e-4, 1.0, 500), [1e-4, 1.0, 0.5, 2.0, 1e-8]])
+    F = O.F(x, O.SIN_RECIP, O.HOST_LIBM)
+    assert (O.F(x, O.SIN_RECIP).view(np.uint64) == F.view(np.uint64)).all()
+    np.savez_compressed(os.path.join(OUT, "sin_bits.npz"), x=x.view(np.uint64), F=F.view(np.uint64))
+    print("sin_bits:", x.size, "points")
+
+
 DEEP_EPS = (("1e-14", 1e-14), ("1e-15", 1e-15), ("1e-16", 1e-16))
 
 
@@ -237,6 +256,7 @@ if __name__ == "__main__":
     if not shutil.which(MPIRUN) and not os.path.exists(MPIRUN):
         print("warning: no mpirun; reference stdout will not be recorded")
     O.build()
-    which = sys.argv[1:] or ["trees", "plugin", "libm_bits", "batch", "deep"]
+    which = sys.argv[1:] or ["trees", "plugin", "libm_bits", "sin_bits", "batch", "deep"]
     for name in which:
-        {"trees": trees, "plugin": plugin, "libm_bits": libm_bits, "batch": batch, "deep": deep}[name]()
+        {"trees": trees, "plugin": plugin, "libm_bits": libm_bits, "sin_bits": sin_bits, "batch": batch,
+         "deep": deep}[name]()

@@ -90,6 +90,33 @@ def test_oracle_vs_host_libm_random(oracle):
     assert np.array_equal(oracle.exp(big).view(np.uint64), oracle.exp(big, oracle.HOST_LIBM).view(np.uint64))
 
 
+def test_oracle_sin_bits_fixture(oracle, sin_bits):
+    """Config 4's F = sin(1.0/x) restated (glibc 2.35 s_sin.c, FMA form) against the committed host
+    libm bits (tests/golden/sin_bits.npz)."""
+    x = sin_bits["x"].view(np.float64)
+    assert np.array_equal(oracle.F(x, oracle.SIN_RECIP).view(np.uint64), sin_bits["F"])
+
+
+@pytest.mark.skipif(not _host_is_glibc_235(), reason="host libm is not glibc 2.35")
+def test_oracle_sin_vs_host_libm_random(oracle):
+    """Every s_sin.c range below 105414350 (the Taylor and table paths, the 0.855..2.426 cosine
+    path, the Cody-Waite reduction), both signs, bit for bit against the host libm."""
+    rng = np.random.default_rng(8)
+    x = np.concatenate([1.0 / rng.uniform(1e-4, 1.0, 1_000_000), rng.uniform(-4.0, 4.0, 500_000),
+                        rng.uniform(-1.05e8, 1.05e8, 300_000), rng.uniform(-0.2, 0.2, 100_000),
+                        rng.uniform(-1e-7, 1e-7, 10_000)])
+    assert np.array_equal(oracle.sin(x).view(np.uint64), oracle.sin(x, oracle.HOST_LIBM).view(np.uint64))
+
+
+def test_sincos_tables_agree():
+    """Oracle table (mpmath) == product table (decimal): two independent generators of glibc's
+    __sincostab."""
+    pat = r"-?0x[0-9a-f.]+p[-+]?\d+"
+    a = [float.fromhex(v) for v in re.findall(pat, open(os.path.join(ROOT, "oracle", "glibc_sincos_table.h")).read())]
+    b = [float.fromhex(v) for v in re.findall(pat, open(os.path.join(ROOT, "ppls_amd", "csrc", "aq_sincos_table.h")).read())]
+    assert len(a) == 444 and a == b
+
+
 def test_exp_tables_agree():
     """Oracle table (mpmath) == product table (decimal): two independent generators of glibc's data."""
     a = re.findall(r"0x[0-9a-f]{16}", open(os.path.join(ROOT, "oracle", "glibc_exp_table.h")).read())
