@@ -210,7 +210,8 @@ __device__ __forceinline__ double cosh_glibc(double x, const ExpEntry* __restric
 // contraction of the source fuses every a*b+c of the polynomials, the cor sums and the Cody-Waite
 // reduction, and the left product of p*a - 0.5*da and x*dx + xx*(...); the __fma_rn()s below spell that
 // out as __fma_rn (this file builds with -ffp-contract=off). The table {sin, cos} of i/128 as double-doubles
-// (aq_sincos_table.h) sits in constant memory: config 4 is one skewed tree, not the bench path.
+// (aq_sincos_table.h, 3.5 KiB) is staged into the kernel's LDS integrand table (stage_f_table) in
+// place of exp's; kSinCosTab is its constant-memory source.
 // Exact for |x| < 105414350 (|arg| > 9.5e-9); beyond that glibc's __branred (Payne-Hanek) is not
 // restated and the device libm's faithful sin answers.
 static __constant__ double kSinCosTab[AQ_SINCOS_TAB_N] = {AQ_SINCOS_TAB_INIT};
@@ -226,7 +227,7 @@ constexpr double big = 0x1.8p45, hp0 = 0x1.921FB54442D18p0, hp1 = 0x1.1A62633145
                  hpinv = 0x1.45F306DC9C883p-1, toint = 0x1.8p52;
 }  // namespace sinc
 
-__device__ __forceinline__ double sin_tab_cos(double x, double dx) {   // s_sin.c do_cos
+__device__ __forceinline__ double sin_tab_cos(double x, double dx, const double* __restrict__ st) {   // s_sin.c do_cos
     using namespace sinc;
     if (x < 0) dx = -dx;
     const double u = big + fabs(x);
@@ -235,12 +236,12 @@ __device__ __forceinline__ double sin_tab_cos(double x, double dx) {   // s_sin.
     const double s = __fma_rn(x * xx, __fma_rn(xx, sn5, sn3), x);
     const double c = xx * __fma_rn(xx, __fma_rn(xx, cs6, cs4), cs2);
     const int k = __double2loint(u) << 2;
-    const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+    const double sn = st[k], ssn = st[k + 1], cs = st[k + 2], ccs = st[k + 3];
     const double cor = __fma_rn(-sn, s, __fma_rn(-cs, c, __fma_rn(-s, ssn, ccs)));
     return cs + cor;
 }
 
-__device__ __forceinline__ double sin_tab_sin(double x, double dx) {   // s_sin.c do_sin
+__device__ __forceinline__ double sin_tab_sin(double x, double dx, const double* __restrict__ st) {   // s_sin.c do_sin
     using namespace sinc;
     const double xold = x;
     if (fabs(x) < 0.126) {                                               // TAYLOR_SIN (x*x, x, dx)
@@ -255,17 +256,17 @@ __device__ __forceinline__ double sin_tab_sin(double x, double dx) {   // s_sin.
     const double s = x + __fma_rn(x * xx, __fma_rn(xx, sn5, sn3), dx);
     const double c = __fma_rn(x, dx, xx * __fma_rn(xx, __fma_rn(xx, cs6, cs4), cs2));
     const int k = __double2loint(u) << 2;
-    const double sn = kSinCosTab[k], ssn = kSinCosTab[k + 1], cs = kSinCosTab[k + 2], ccs = kSinCosTab[k + 3];
+    const double sn = st[k], ssn = st[k + 1], cs = st[k + 2], ccs = st[k + 3];
     const double cor = __fma_rn(cs, s, __fma_rn(-sn, c, __fma_rn(s, ccs, ssn)));
     return copysign(sn + cor, xold);
 }
 
-__device__ __forceinline__ double sin_glibc(double x) {
+__device__ __forceinline__ double sin_glibc(double x, const double* __restrict__ st) {
     using namespace sinc;
     const unsigned k = (unsigned)__double2hiint(x) & 0x7fffffffu;
     if (k < 0x3e500000u) return x;                                       // |x| < 2^-26
-    if (k < 0x3feb6000u) return sin_tab_sin(x, 0.0);                     // |x| < 0.855469
-    if (k < 0x400368fdu) return copysign(sin_tab_cos(hp0 - fabs(x), hp1), x);   // |x| < 2.426265
+    if (k < 0x3feb6000u) return sin_tab_sin(x, 0.0, st);                     // |x| < 0.855469
+    if (k < 0x400368fdu) return copysign(sin_tab_cos(hp0 - fabs(x), hp1, st), x);   // |x| < 2.426265
     if (k < 0x419921fbu) {                                               // |x| < 105414350
         const double t = __fma_rn(x, hpinv, toint);
         const double xn = t - toint;
@@ -277,11 +278,14 @@ __device__ __forceinline__ double sin_glibc(double x) {
         t1 = xn * pp4;
         const double b = t2 - t1;
         db += (t2 - b) - t1;
-        const double r = (n & 1) ? sin_tab_cos(b, db) : sin_tab_sin(b, db);
+        const double r = (n & 1) ? sin_tab_cos(b, db, st) : sin_tab_sin(b, db, st);
         return (n & 2) ? -r : r;
     }
     return sin(x);                                                       // __branred range, inf, nan
 }
+
+// A kernel's integrand table as __sincostab (its LDS copy, stage_f_table).
+__device__ __forceinline__ const double* sin_table(const ExpEntry* tab) { return reinterpret_cast<const double*>(tab); }
 
 // Integrand ids (include/aquad.h aq_integrand).
 enum : int { F_COSH4 = 0, F_SIN_RECIP = 1, F_USER = 2 };
@@ -313,7 +317,7 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
     } else if constexpr (FID == F_USER) {
         return user::F(x, tab);
     } else {
-        return sin_glibc(1.0 / x);   // SURVEY config 4: sin(1.0/(arg)) with glibc's sin
+        return sin_glibc(1.0 / x, sin_table(tab));   // config 4: sin(1.0/(arg)); tab: stage_f_table
     }
 }
 
@@ -495,15 +499,31 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
         for (int k = 0; k < K; ++k) f[k] = user::F(x[k], tab);
     } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) f[k] = sin_glibc(1.0 / x[k]);
+        for (int k = 0; k < K; ++k) f[k] = sin_glibc(1.0 / x[k], sin_table(tab));
     }
 }
+
+// A kernel's LDS integrand table: glibc exp's 128 entries (cosh^4 and the plug-ins), or for sin(1/x)
+// glibc's __sincostab (444 doubles in 222 16-B entries) -- integrand<F_SIN_RECIP> reads `tab` as that.
+template <int FID>
+constexpr int ftab_entries() { return FID == F_SIN_RECIP ? (AQ_SINCOS_TAB_N + 1) / 2 : 128; }
 
 // Stage the exp table into LDS (call from every thread, then __syncthreads()).
 __device__ __forceinline__ void stage_exp_table(ExpEntry* lds, const ExpPair* __restrict__ g) {
     for (int i = threadIdx.x; i < 128; i += blockDim.x) {
         lds[i].tail_bits = g[i].tail_bits;
         lds[i].sbits = g[i].sbits;
+    }
+}
+
+// Stage FID's integrand table (ftab_entries<FID>() entries) into LDS; then __syncthreads().
+template <int FID>
+__device__ __forceinline__ void stage_f_table(ExpEntry* lds, const ExpPair* __restrict__ g) {
+    if constexpr (FID == F_SIN_RECIP) {
+        double* const d = reinterpret_cast<double*>(lds);
+        for (int i = threadIdx.x; i < AQ_SINCOS_TAB_N; i += blockDim.x) d[i] = kSinCosTab[i];
+    } else {
+        stage_exp_table(lds, g);
     }
 }
 

@@ -123,6 +123,7 @@ constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from
 // launches of fewer integrals keep per-workgroup (per-CU) counts and LDS exact accumulators (the LDS
 // left beside the pair block holds 12)
 constexpr int PCU_MAXK = 12;
+constexpr int PCU_ROW = PCU_MAXK - 1;   // per-CU LDS rows: tags < k < PCU_MAXK
 constexpr int STATIC_MAXK = 16;     // launches of fewer integrals (unsharded): one share per wave, static stride
 constexpr int MAXK = 65536;         // max integrals per launch (tag: the pair word's high 16 bits)
 // The pair word dt: bits 0-7 the pair's depth (the depth of its two tasks), bit 8 SPAN_BIT, bits
@@ -533,8 +534,8 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
             atomicAdd(&S.tasks, (unsigned long long)t);
             if constexpr (PCU) {
                 atomicAdd(&pc[tag], (unsigned long long)t);
-                atomicAdd(&pc[PCU_MAXK + tag], (unsigned long long)l);
-                atomicMax(&pc[2 * PCU_MAXK + tag], (unsigned long long)m);
+                atomicAdd(&pc[PCU_ROW + tag], (unsigned long long)l);
+                atomicMax(&pc[2 * PCU_ROW + tag], (unsigned long long)m);
                 xs_atomic_add(px[tag].limb, hi);
                 xs_atomic_add(px[tag].limb, lo);
             } else {
@@ -779,10 +780,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     double* const s_fa = s_pr + 2 * LREC;
     double* const s_fm = s_pr + 3 * LREC;
     double* const s_fb = s_pr + 4 * LREC;
-    __shared__ ExpEntry tab[128];
+    __shared__ ExpEntry tab[ftab_entries<FID>()];   // exp's, or sin(1/x)'s __sincostab (stage_f_table)
     __shared__ WgState S;
-    __shared__ unsigned long long s_pc[PCU ? 3 * PCU_MAXK : 1];
-    __shared__ XSum s_px[PCU ? PCU_MAXK : 1];
+    __shared__ unsigned long long s_pc[PCU ? 3 * PCU_ROW : 1];
+    __shared__ XSum s_px[PCU ? PCU_ROW : 1];
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
 
     const unsigned tid = threadIdx.x;
@@ -800,7 +801,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // rings' harmless pairs among them): their latency, a cold HBM read at every launch, overlaps
     // the set-up instead of preceding it
     ExpPair tv{};
-    if (tid < 128u) tv = P.gtab[tid];
+    if (FID != F_SIN_RECIP && tid < 128u) tv = P.gtab[tid];
+    static_assert(AQ_SINCOS_TAB_N <= PT, "one sin-table entry per thread");
+    double sv = 0.0;
+    if (FID == F_SIN_RECIP && tid < (unsigned)AQ_SINCOS_TAB_N) sv = kSinCosTab[tid];
     {
         const unsigned b0 = (tid >> 6) * WCAP;
         for (unsigned i = lane_id(); i < (unsigned)WCAP; i += 64) {
@@ -809,7 +813,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
     }
 #else
-    stage_exp_table(tab, P.gtab);
+    stage_f_table<FID>(tab, P.gtab);
 #endif
     if (bid == 0)
         for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
@@ -817,14 +821,16 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1;
         S.exited = 0; S.tasks = 0;
     }
-    if (PCU && tid < 3u * PCU_MAXK) s_pc[tid] = 0ull;
+    if (PCU && tid < 3u * PCU_ROW) s_pc[tid] = 0ull;
     if (PCU)
-        for (unsigned i = tid; i < (unsigned)(PCU_MAXK * XS_LIMBS); i += PT) s_px[i / XS_LIMBS].limb[i % XS_LIMBS] = 0;
+        for (unsigned i = tid; i < (unsigned)(PCU_ROW * XS_LIMBS); i += PT) s_px[i / XS_LIMBS].limb[i % XS_LIMBS] = 0;
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
 #if AQ_PRO_OVERLAP
-    if (tid < 128u) {
+    if (FID == F_SIN_RECIP) {
+        if (tid < (unsigned)AQ_SINCOS_TAB_N) reinterpret_cast<double*>(tab)[tid] = sv;
+    } else if (tid < 128u) {
         tab[tid].tail_bits = tv.tail_bits;
         tab[tid].sbits = tv.sbits;
     }
@@ -1942,8 +1948,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned cu = cu_slot();
             for (int p = 0; p < P.nprob; ++p) {
                 const unsigned long long t = __hip_atomic_load(&s_pc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const unsigned long long l = __hip_atomic_load(&s_pc[PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const unsigned m = (unsigned)__hip_atomic_load(&s_pc[2 * PCU_MAXK + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned long long l = __hip_atomic_load(&s_pc[PCU_ROW + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const unsigned m = (unsigned)__hip_atomic_load(&s_pc[2 * PCU_ROW + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 unsigned long long* wp = P.parts + 2 * ((size_t)(P.first_slot + p) * gridDim.x + bid);
                 wp[0] = pack_cu(t, cu);
                 wp[1] = (l << 8) | (unsigned long long)(m & 255u);

@@ -64,8 +64,9 @@ struct DevResults {
 template <int FID, bool COSH_ONLY>
 __global__ __launch_bounds__(256) void k_eval(const double* __restrict__ x, double* __restrict__ out, size_t n,
                                               const ExpPair* __restrict__ gtab) {
-    __shared__ ExpEntry tab[128];
-    stage_exp_table(tab, gtab);
+    constexpr int TF = COSH_ONLY ? F_COSH4 : FID;
+    __shared__ ExpEntry tab[ftab_entries<TF>()];
+    stage_f_table<TF>(tab, gtab);
     __syncthreads();
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
     if constexpr (FID == F_COSH4 && !COSH_ONLY) {
@@ -93,8 +94,8 @@ struct Rec {
 
 template <int FID>
 __global__ __launch_bounds__(64) void k_root(double a, double b, Rec* out, const ExpPair* __restrict__ gtab) {
-    __shared__ ExpEntry tab[128];
-    stage_exp_table(tab, gtab);
+    __shared__ ExpEntry tab[ftab_entries<FID>()];
+    stage_f_table<FID>(tab, gtab);
     __syncthreads();
     if (threadIdx.x == 0) {
         Rec r;
@@ -111,10 +112,10 @@ __global__ __launch_bounds__(256) void k_level(const Rec* __restrict__ in, unsig
                                                unsigned* __restrict__ n_out, unsigned cap_out, double eps, int depth,
                                                int max_depth, DevResults* __restrict__ res,
                                                const ExpPair* __restrict__ gtab) {
-    __shared__ ExpEntry tab[128];
+    __shared__ ExpEntry tab[ftab_entries<FID>()];
     __shared__ double s_area[4];
     __shared__ unsigned s_cnt[2][4];
-    stage_exp_table(tab, gtab);
+    stage_f_table<FID>(tab, gtab);
     __syncthreads();
     double area = 0.0;
     unsigned tasks = 0, leaves = 0;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ 
     // chained levels: the count a previous step appended (read once; uniform), clamped to n_in = the
     // host's bound (<= the input buffer's capacity; a count beyond it was flagged as an overflow)
     if (n_in_dev) n_in = min(*n_in_dev, n_in);
-    __shared__ ExpEntry tab[128];
+    __shared__ ExpEntry tab[ftab_entries<FID>()];
     __shared__ double s_h[LEVEL_NW], s_l[LEVEL_NW];
     __shared__ unsigned s_t[LEVEL_NW], s_a[LEVEL_NW], s_e[LEVEL_NW];
     __shared__ unsigned s_wc[2][LEVEL_NW], s_base[2];
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ 
         }
     };
     if (AQ_LEVEL_HOIST && blockIdx.x * chunk < n_in) load_chunk(blockIdx.x * chunk);
-    stage_exp_table(tab, gtab);
+    stage_f_table<FID>(tab, gtab);
     __syncthreads();
     double hi = 0.0, lo = 0.0;
     unsigned tasks = 0, leaves = 0, err = 0;
@@ -387,12 +388,12 @@ __global__ __launch_bounds__(NARROW_T) void k_level_narrow(Rec* __restrict__ buf
                                                            int max_depth, double* __restrict__ acc,
                                                            const ExpPair* __restrict__ gtab) {
     constexpr int NWV = NARROW_T / 64;
-    __shared__ ExpEntry tab[128];
+    __shared__ ExpEntry tab[ftab_entries<FID>()];
     __shared__ unsigned s_wc[NWV];
     __shared__ unsigned s_n;
     __shared__ double s_h[NWV], s_l[NWV];
     __shared__ unsigned s_t[NWV], s_a[NWV], s_e[NWV], s_v[NWV];
-    stage_exp_table(tab, gtab);
+    stage_f_table<FID>(tab, gtab);
     if (threadIdx.x == 0) s_n = min(counts[d0], cap);
     __syncthreads();
     double hi = 0.0, lo = 0.0;
@@ -473,8 +474,8 @@ __global__ __launch_bounds__(NARROW_T) void k_level_narrow(Rec* __restrict__ buf
 
 template <int FID>
 __global__ __launch_bounds__(64) void k_frontier_root(double a, double b, Rec* out, const ExpPair* __restrict__ gtab) {
-    __shared__ ExpEntry tab[128];
-    stage_exp_table(tab, gtab);
+    __shared__ ExpEntry tab[ftab_entries<FID>()];
+    stage_f_table<FID>(tab, gtab);
     __syncthreads();
     if (threadIdx.x == 0) out[0] = Rec{a, b, integrand<FID>(a, tab), integrand<FID>(b, tab)};
 }
