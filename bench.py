@@ -7,12 +7,26 @@ of B (default 32768) such integrals through the hot path (persistent on-device f
 ppls_amd/csrc/aq_stream.h). With N ranks (one process per GPU, torch.distributed backend "nccl" =
 RCCL) every integral is sharded: rank r evaluates shard r of N of each integral (the domain split
 into subranges per GPU; strong scaling, total work fixed), and a rank packs up to N batches into
-one persistent launch so a launch holds the same work whatever N. The partial results of the K
+one persistent launch (up to the 65536 integrals a launch holds). The partial results of the K
 timed steps are combined with ONE all-reduce inside the timed region. Launches are pipelined
-(no host sync between them); every integral's counts are verified bit-exactly against the golden
-tree after timing.
+(no host sync between them); every integral's counts are verified bit-exactly and its area to
+1e-12 relative against the golden tree after timing.
+
+After the headline's timed region, two secondary passes are timed the same way (barrier + sync on
+both sides, max over ranks) and reported under "secondary":
+  * C3 (BASELINE configs[2]): 1 000 000 splitmix64-bounded integrals at EPSILON=1e-10, split into
+    contiguous whole-integral blocks per rank, through the batch front end (aq_integrate_batch);
+    verified by T = 2L - 1 for every integral, the committed per-integral prefix and the exact KAT
+    (Σ leaves of the first 10 000 draws, tests/golden/batch.json);
+  * C5 (BASELINE configs[4]): EPSILON=1e-12, 4096 copies of the integral per pass, each sharded over
+    the N GPUs; verified against the golden tree (counts exact, area to 1e-12).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--eps E] [--no-cpu-baseline]
+
+--gpus N > 1 with no launcher (WORLD_SIZE unset): this process times the CPU baseline first (no GPU
+call), then runs N ranks itself through `torch.distributed.run` and exits with their status. Under a
+launcher WORLD_SIZE must equal --gpus (aquadPartA.c:86-90: the process count is the launch's, and a
+mismatch is an error, not a fallback).
 
 Prints ONE JSON line (rank 0). `value` = accepted subintervals/s over all GPUs; roofline is the
 persistent kernel's FP64 rate (38 algorithmic FLOP per task) over its HIP-event
@@ -22,6 +36,7 @@ reference's bag of tasks restated on threads (oracle/aq_bag.c) timed on this hos
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -31,7 +46,17 @@ sys.path.insert(0, ROOT)
 
 FLOP_PER_TASK = 38          # exp 20 + cosh tail 3 + pow4 3 + step 12
 FP64_PEAK = 78.6e12         # MI355X FP64 vector peak (256 CU x 2.4 GHz x 128 FLOP/clk), MI355X_MICROARCH.md
-GOLDEN = {1e-10: (1464273, 732137), 1e-12: (6606491, 3303246), 1e-8: (319295, 159648), 1e-3: (6567, 3284)}
+# eps -> (tasks, accepted, quad-precision Σ of the leaf areas) of cosh4 on [0,5] (tests/golden/trees.json,
+# pinned by the reference binary's own runs)
+GOLDEN = {1e-10: (1464273, 732137, 7583461.361505481304452902),
+          1e-12: (6606491, 3303246, 7583461.361497082882355142),
+          1e-8: (319295, 159648, 7583461.361685127681076307),
+          1e-3: (6567, 3284, 7583461.801486495444390989)}
+AREA_RTOL = 1e-12           # the north star's area tolerance
+C3_N = 1_000_000
+C5_COPIES = 4096
+SPLITMIX_GOLDEN = 0x9E3779B97F4A7C15
+CPU_ENV = "BENCH_CPU_BASELINE"   # the launcher's CPU baseline, handed to rank 0 (JSON)
 
 
 def host_cores():
@@ -54,7 +79,7 @@ def cpu_baseline(eps, target_s=12.0):
     dispatch loop and task body over the host libm), with P = the cores this process may load. Its
     totals must equal the reference's. (The reference binary itself is timed in the build container,
     BASELINE.md; it is not shipped here.) Falls back to the sequential oracle restatement."""
-    tasks_golden, leaves_golden = GOLDEN.get(eps, (None, None))
+    tasks_golden, leaves_golden = GOLDEN.get(eps, (None, None, None))[:2]
     ncpu, nprocs = host_cores()
     bag = os.path.join(ROOT, "oracle", "_build", "aq_bag")
     if os.path.exists(bag) and leaves_golden and eps in (1e-3, 1e-10, 1e-12):
@@ -90,16 +115,20 @@ def cpu_baseline(eps, target_s=12.0):
                                       f"{t_total:.1f} s"}
 
 
-def load_traffic(tasks_per_launch):
-    """HBM bytes per launch of the persistent kernel: the committed PMC profile's bytes per task
-    (profiles/pmc_traffic.json, tools/profile_round.sh) times this launch's tasks (or None)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_json(rel):
     try:
-        with open(p) as f:
-            per_task = json.load(f).get("hbm_bytes_per_task")
-        return per_task * tasks_per_launch if per_task else None
+        with open(os.path.join(ROOT, rel)) as f:
+            return json.load(f)
     except Exception:
         return None
+
+
+def load_traffic(tasks_per_launch):
+    """HBM bytes per launch of the persistent kernel: the committed PMC profile's bytes per task
+    (profiles/pmc_traffic.json, tools/profile_round.sh) times this launch's tasks (or None). Not
+    measured in this run: PMC counters need their own profiler passes."""
+    per_task = (load_json(os.path.join("profiles", "pmc_traffic.json")) or {}).get("hbm_bytes_per_task")
+    return per_task * tasks_per_launch if per_task else None
 
 
 def ranks_seen(dist, coll, distributed):
@@ -132,11 +161,39 @@ def rank_stats(dist, coll, distributed, kern_ms, launches, tasks, elapsed):
             "task_imbalance": max(tk) / mean(tk) if mean(tk) > 0 else None}
 
 
+def areas_ok(areas, want):
+    """Every area within AREA_RTOL (relative) of the golden quad Σ."""
+    import numpy as np
+    return bool(np.all(np.abs(np.asarray(areas, np.float64) - want) <= AREA_RTOL * abs(want)))
+
+
+def splitmix64_bounds(n):
+    """state += golden; standard mix; u = (z >> 11) * 2^-53; a = 5u1, b = 5u2, swap."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        k = np.arange(1, 2 * n + 1, dtype=np.uint64)
+        z = np.uint64(SPLITMIX_GOLDEN) + k * np.uint64(SPLITMIX_GOLDEN)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    a, b = 5.0 * u[0::2], 5.0 * u[1::2]
+    return np.minimum(a, b), np.maximum(a, b)
+
+
+def ceiling():
+    """The same-occupancy ceiling of the kernel's own arithmetic (committed microbenchmark, the
+    kernel's per-pair code on register-held pairs: profiles/ceiling.json), or None."""
+    return load_json(os.path.join("profiles", "ceiling.json"))
+
+
 def bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, per_launch, ctx_cus, single_ms,
-               single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu, cu_stats=None):
+               single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu, cu_stats=None,
+               secondary=None, checks=None):
     """The one JSON line rank 0 prints (the driver's contract plus roofline, cpu_baseline and the
     multi-rank fields: backend, ranks_seen -- counted by a collective -- and per-rank kernel time and
     tasks with their imbalance)."""
+    ceil = ceiling()
     return {
         "metric": "accepted subintervals/sec + FP64 F-evals/sec at 1/2/4/8 MI355X, EPSILON=1e-10",
         "value": accepted_total / elapsed,
@@ -159,22 +216,54 @@ def bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, 
                    "parallelism": f"shard{world}" if world > 1 else "single-gpu",
                    "integrals_per_step": B,
                    "integrals_per_launch": per_launch,
+                   # a launch of m shards of 1/N of an integral each holds m / N integrals' work
+                   "integral_equivalents_per_launch": per_launch / world,
                    "workgroups_per_gpu": ctx_cus},
         "single_integral_kernel_us": single_ms * 1e3 / single_n if single_n else None,
         "verified": ok,
+        "checks": checks,
         "backend": backend,
         "ranks_seen": seen,
         "per_rank": stats,
         "tasks_per_cu": cu_stats,
         "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK, "traffic": load_traffic(tasks_per_launch),
+                     "traffic_source": "not measured in this run: profiles/pmc_traffic.json's PMC bytes per task "
+                                       "(FETCH_SIZE x2 + WRITE_SIZE passes) x this launch's tasks",
+                     "ceiling": (ceil or {}).get("frac"), "ceiling_source": (ceil or {}).get("source"),
                      "kernel": "aq::k_stream<0,false,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
                      "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": tasks_per_launch},
         "cpu_baseline": cpu,
+        "secondary": secondary,
     }
 
 
-def main():
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(n, argv, port):
+    """One rank per GPU of this node (the driver's own launch line)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(args, argv, runner=None, baseline=cpu_baseline):
+    """--gpus N > 1 without a launcher: time the CPU baseline here (this process makes no GPU call),
+    run N ranks as a child `torch.distributed.run`, hand the baseline to rank 0 through the
+    environment, and return the children's exit status (non-zero if any rank failed)."""
+    env = dict(os.environ)
+    if not args.no_cpu_baseline:
+        env[CPU_ENV] = json.dumps(baseline(args.eps))
+    runner = runner or (lambda cmd, env: subprocess.call(cmd, env=env))
+    return runner(launcher_cmd(args.gpus, argv, free_port()), env)
+
+
+def parse(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8, help="timed batches")
@@ -186,21 +275,33 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true",
                     help="skip the one-integral-per-launch latency probe (profiling runs: every dispatch is K-wide)")
-    args = ap.parse_args()
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C3 / C5 passes after the headline")
+    ap.add_argument("--c3-n", type=int, default=C3_N, help="integrals of the C3 pass")
+    return ap.parse_args(argv)
 
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     # launched by torch.distributed.run (even with one rank): a process group, so the combine below
     # runs through RCCL; a plain `python bench.py` is the single-GPU run with no group
     distributed = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
-    if world != args.gpus:
-        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
-    # CPU baseline first: before this process touches the GPU (child processes only).
+    # CPU baseline first: before this process touches the GPU (child processes only). Handed over by
+    # this script's own launcher, else timed by rank 0 here (the other ranks wait in the rendezvous).
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.eps)
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = json.loads(os.environ[CPU_ENV]) if os.environ.get(CPU_ENV) else cpu_baseline(args.eps)
 
     import numpy as np
     import torch
@@ -226,6 +327,11 @@ def main():
             if h is not t:
                 t.copy_(h)
 
+    def reduce_list(vals, op):
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        all_reduce(t, op)
+        return t.cpu().tolist()
+
     backend = dist.get_backend() if distributed else None
     seen = ranks_seen(dist, coll, distributed)
     if seen != world:
@@ -233,38 +339,42 @@ def main():
 
     ctx = Context(dev)
     ctx.set_level_histograms(False)
-    problem = Problem(eps=args.eps)
     nslots = ctx.async_slots
 
     def barrier():
         if distributed:
             dist.barrier()
 
-    B = args.batch
-    if B < 1 or B > min(ctx.max_integrals_per_launch, nslots):
-        raise SystemExit(f"--batch must be in [1, {min(ctx.max_integrals_per_launch, nslots)}]")
-    # batches per launch: N of them (each rank holds 1/N of every integral), within the slot budget
-    lb = max(1, min(world, min(ctx.max_integrals_per_launch, nslots) // B))
-
-    def launch(m):
-        # m integrals of the workload in one persistent launch (slots 0..m-1), this rank's shard
+    def in_turn(fn):
+        """Run fn on this rank; in the shared-GPU rehearsal the ranks take turns (persistent grids
+        need the whole GPU), each finishing before the next starts."""
         if shared and world > 1:
-            # rehearsal: persistent grids need the whole GPU, so the ranks sharing it take turns
+            out = None
             for r in range(world):
                 if r == rank:
-                    ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank,
-                                             nshards=world)
+                    out = fn()
                     ctx.synchronize()
                 dist.barrier()
-            return
-        ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), args.eps, first_slot=0, shard=rank, nshards=world)
+            return out
+        return fn()
+
+    B = args.batch
+    cap = min(ctx.max_integrals_per_launch, nslots)
+    if B < 1 or B > cap:
+        raise SystemExit(f"--batch must be in [1, {cap}]")
+    # batches per launch: N of them (each rank holds 1/N of every integral), within the slot budget
+    lb = max(1, min(world, cap // B))
+
+    def launch(m, eps=args.eps):
+        # m integrals of the workload in one persistent launch (slots 0..m-1), this rank's shard
+        in_turn(lambda: ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), eps, first_slot=0, shard=rank,
+                                                 nshards=world))
 
     # single-integral latency (one integral per launch), reported beside the throughput: on one GPU
     # the kernel of the synchronous call a user makes for one integral (aq_integrate: its result slot
     # is re-zeroed by the fetch, so nothing is enqueued before the launch), on N the rank's shard
     single_ms, single_n = 0.0, 0
     if not args.no_single:
-        from ppls_amd import Problem
         one = (lambda: ctx.integrate(Problem(eps=args.eps))) if world == 1 else (lambda: launch(1))
         one()                         # untimed: the first K=1 launch pays the K=1 setup
         ctx.synchronize()
@@ -312,9 +422,7 @@ def main():
     stats = rank_stats(dist, coll if distributed else "cpu", distributed, kern_ms, launches, float(my_tasks.item()),
                        elapsed)
     if distributed:
-        tt = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
-        all_reduce(tt, dist.ReduceOp.MAX)
-        elapsed, kern_avg_ms = float(tt[0]), float(tt[1])
+        elapsed, kern_avg_ms = reduce_list([elapsed, kern_ms / max(launches, 1)], dist.ReduceOp.MAX)
     else:
         kern_avg_ms = kern_ms / max(launches, 1)
     per_launch = n_int / max(launches, 1)
@@ -326,12 +434,17 @@ def main():
                 "imbalance": (max(cu_v) * len(cu_v) / sum(cu_v)) if cu_v and sum(cu_v) else None,
                 "sum": sum(cu_v)}
 
-    # verify every timed step against the golden tree
+    # verify every timed step against the golden tree: counts exact, areas to AREA_RTOL
     tot = totals.cpu().numpy()
-    tg, lg = GOLDEN.get(args.eps, (None, None))
-    ok = bool((tot[:, 3] == 0).all()) and seen == world and cu_stats["sum"] == int(my_tasks.item())
+    tg, lg, ag = GOLDEN.get(args.eps, (None, None, None))
+    checks = {"errors": bool((tot[:, 3] == 0).all()), "ranks": seen == world,
+              "cu_counters": cu_stats["sum"] == int(my_tasks.item())}
     if tg is not None:
-        ok = ok and bool((tot[:, 1] == tg).all() and (tot[:, 2] == lg).all())
+        checks["counts"] = bool((tot[:, 1] == tg).all() and (tot[:, 2] == lg).all())
+        checks["areas"] = areas_ok(tot[:, 0], ag)
+    # every rank's view (the per-CU check is per rank)
+    checks = dict(zip(checks, (bool(v) for v in reduce_list([float(v) for v in checks.values()], dist.ReduceOp.MIN))))
+    ok = all(checks.values())
     accepted_total = float(tot[:, 2].sum())
     tasks_total = float(tot[:, 1].sum())
     f_evals = tasks_total + 2 * n_int   # algorithmic F evaluations: 1 per task + F(A), F(B) per integral
@@ -341,16 +454,111 @@ def main():
     tasks_per_launch = mine.tasks * per_launch
     achieved = FLOP_PER_TASK * tasks_per_launch / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
 
+    secondary = None
+    if not args.no_secondary:
+        secondary = [
+            c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist),
+            c5_pass(ctx, rank, world, barrier, launch, reduce_list, dist, torch, all_reduce),
+        ]
+        ok = ok and all(s["verified"] for s in secondary)
+
     if rank == 0:
         out = bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, per_launch, ctx.num_cus,
                          single_ms, single_n, ok, backend, seen, stats, achieved, kern_avg_ms, tasks_per_launch, cpu,
-                         cu_stats)
+                         cu_stats, secondary, checks)
         print(json.dumps(out))
     ctx.close()
     if distributed:
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)
+
+
+def c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist):
+    """BASELINE configs[2]: 1 M splitmix64-bounded integrals at EPSILON=1e-10, contiguous whole-integral
+    blocks per rank through aq_integrate_batch (65536 integrals per persistent launch)."""
+    import numpy as np
+    import torch
+    eps = 1e-10
+    n = args.c3_n
+    a, b = splitmix64_bounds(n)
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    # untimed: one launch of this workload sizes the jobs of the next (the launch-to-launch hint)
+    w = min(hi - lo, 65536)
+    in_turn(lambda: ctx.integrate_batch(a[lo:lo + w], b[lo:lo + w], eps))
+    ctx.kernel_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    area, tasks, acc = in_turn(lambda: ctx.integrate_batch(a[lo:hi], b[lo:hi], eps))
+    barrier()
+    t1 = time.perf_counter()
+    kern_ms, launches = ctx.kernel_time()
+    ctx.kernel_timing(False)
+    ok = bool((tasks == 2 * acc - 1).all())
+    golden = load_json(os.path.join("tests", "golden", "batch.json")) or {}
+    checked = []
+    if lo == 0:
+        pre = golden.get("leaves_eps1e-10") or []
+        m = min(len(pre), hi)
+        if m:
+            ok = ok and bool((acc[:m] == np.asarray(pre[:m], np.uint64)).all())
+            want = np.array([float.fromhex(v) for v in golden["area_eps1e-10_hex"][:m]])
+            ok = ok and bool(np.all(np.abs(area[:m] - want) <= AREA_RTOL * np.abs(want)))
+            checked.append(f"counts and areas of integrals 0..{m - 1} vs tests/golden/batch.json")
+        kn = golden.get("kat_n_eps1e-10", 0)
+        if kn and hi >= kn:
+            ok = ok and int(acc[:kn].sum()) == golden["kat_sum_leaves_eps1e-10"] \
+                and int(tasks[:kn].sum()) == golden["kat_sum_tasks_eps1e-10"]
+            checked.append(f"exact Σ leaves / tasks of the first {kn} draws (mean leaves "
+                           f"{golden['kat_sum_leaves_eps1e-10'] / kn:.4f})")
+    # every rank's accepted / tasks / kernel seconds / verdict summed, the wall time's max
+    leaves, tsum, ksum, okall = reduce_list([float(acc.sum()), float(tasks.sum()), kern_ms / 1e3, 1.0 if ok else 0.0],
+                                            dist.ReduceOp.SUM)
+    elapsed, = reduce_list([t1 - t0], dist.ReduceOp.MAX)
+    return {"workload": "C3 (BASELINE configs[2]): %d splitmix64-bounded cosh4 integrals at EPSILON=1e-10, "
+                        "whole integrals in contiguous blocks per rank" % n,
+            "value": leaves / elapsed, "unit": "accepted subintervals/s", "ms": elapsed * 1e3,
+            "integrals_per_s": n / elapsed, "accepted": int(leaves), "tasks": int(tsum),
+            "frac": FLOP_PER_TASK * tsum / ksum / FP64_PEAK if ksum > 0 else None,
+            "verified": okall == world, "checks": ["T = 2L - 1 for every integral"] + checked}
+
+
+def c5_pass(ctx, rank, world, barrier, launch, reduce_list, dist, torch, all_reduce):
+    """BASELINE configs[4]: EPSILON=1e-12, C5_COPIES copies of cosh4 on [0,5] in one launch, each
+    integral sharded over the N GPUs; one untimed launch sizes the jobs, two are timed."""
+    eps = 1e-12
+    m = C5_COPIES
+    launch(m, eps)                      # untimed
+    ctx.synchronize()
+    reps = 2
+    totals = torch.zeros((reps * m, 4), dtype=torch.float64, device="cuda")
+    ctx.kernel_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        launch(m, eps)
+        ctx.gather_results(0, m, totals.data_ptr() + i * m * 4 * totals.element_size())
+    ctx.synchronize()
+    all_reduce(totals, dist.ReduceOp.SUM)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    kern_ms, launches = ctx.kernel_time()
+    ctx.kernel_timing(False)
+    tot = totals.cpu().numpy()
+    tg, lg, ag = GOLDEN[eps]
+    ok = bool((tot[:, 3] == 0).all() and (tot[:, 1] == tg).all() and (tot[:, 2] == lg).all()) and areas_ok(tot[:, 0], ag)
+    elapsed, = reduce_list([t1 - t0], dist.ReduceOp.MAX)
+    ksum, okall = reduce_list([kern_ms / 1e3, 1.0 if ok else 0.0], dist.ReduceOp.SUM)
+    ok = okall == world
+    tasks = float(tot[:, 1].sum())
+    return {"workload": "C5 (BASELINE configs[4]): cosh4 on [0,5] at EPSILON=1e-12, %d copies per launch, each "
+                        "sharded over the %d GPU(s), %d timed launches" % (m, world, reps),
+            "value": float(tot[:, 2].sum()) / elapsed, "unit": "accepted subintervals/s", "ms": elapsed * 1e3,
+            "frac": FLOP_PER_TASK * tasks / ksum / FP64_PEAK if ksum > 0 else None,
+            "verified": ok, "checks": ["counts exact and areas to 1e-12 vs the golden tree, every copy"]}
 
 
 if __name__ == "__main__":

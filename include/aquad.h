@@ -35,6 +35,8 @@ extern "C" {
 #define AQ_ENOMEM (-6)     /* device or host allocation failed */
 #define AQ_ENODEV (-7)     /* no HIP device */
 #define AQ_ERCCL (-8)      /* an RCCL call failed (aq_group_*) */
+#define AQ_ERESIDENT (-9)  /* the persistent grid cannot be co-resident on the device (its workgroups wait
+                            on each other): refused before launch, never a stall */
 
 #define AQ_DEFAULT_MAX_DEPTH 96
 #define AQ_MAX_LEVELS 128     /* length of the per-level histograms */
@@ -95,6 +97,11 @@ int aq_ctx_device_bytes(const aq_ctx *ctx, uint64_t *bytes);
 /* Per-level task/accepted histograms on the persistent path (default on; a diagnostic the
  * reference does not produce -- pipelined callers switch it off). */
 int aq_set_level_histograms(aq_ctx *ctx, int enable);
+/* The persistent kernel's grid is one workgroup per CU (AQ_GRID=<n> in the environment at create time
+ * overrides it, e.g. to leave CUs to other work). Its workgroups hand work to each other, so every
+ * launch checks -- for the exact kernel instance, block size and LDS -- that the device can hold the
+ * whole grid at once, and refuses with AQ_ERESIDENT otherwise. AQ_COOP=1 at create time launches it
+ * as a cooperative kernel (the runtime's own co-residency guarantee) instead of a plain launch. */
 /* How long a waiting workgroup tolerates NO PROGRESS of the on-device work queue before the launch
  * fails with AQ_ETIMEOUT (default 10 s, or the AQ_STALL_MS environment variable at create time). A
  * bound on stalls, not on run time: launches of any length that keep progressing never time out. */

@@ -96,9 +96,6 @@ __host__ __device__ constexpr double f_scale() { return FID == F_COSH4 ? 16.0 : 
 template <int FID>
 __host__ __device__ constexpr double area_scale() { return doubled_areas<FID>() ? 0.5 / f_scale<FID>() : 1.0; }
 
-#ifndef AQ_EARLY_STEP
-#define AQ_EARLY_STEP 1   // r02 A/B: 27.25 -> 27.04 ms per 8192-integral launch
-#endif
 template <int FID, int K>
 __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (&r)[K], const double (&fl)[K],
                                             const double (&fr)[K], double eps2, const ExpEntry* __restrict__ tab,
@@ -107,9 +104,8 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
     double mid[K], fmid[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) mid[k] = (l[k] + r[k]) / 2;   // :187
-#if AQ_EARLY_STEP
     // the parts of the step that do not need F(mid) first: independent work the scheduler can
-    // place in the latency gaps of the F chains
+    // place in the latency gaps of the F chains (r02 A/B: 27.25 -> 27.04 ms per 8192-integral launch)
     double lr2e[K], wl[K], wr[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -119,20 +115,13 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
         // computed HERE (volatile: not sunk below the F chains' range-check branch)
         asm volatile("" : "+v"(lr2e[k]), "+v"(wl[k]), "+v"(wr[k]));
     }
-#endif
     integrand_k<FID, K, (f_scale<FID>() != 1.0)>(mid, fmid, tab, kk, range_hint, out_mask);   // :188 (f_scale F)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         if constexpr (doubled_areas<FID>()) {
-#if AQ_EARLY_STEP
             const double lr2 = lr2e[k];                                   // 2 * lrarea, :185
             const double l2 = (fl[k] + fmid[k]) * wl[k];                  // 2 * larea,  :189
             const double r2 = (fmid[k] + fr[k]) * wr[k];                  // 2 * rarea,  :190
-#else
-            const double lr2 = (fl[k] + fr[k]) * (r[k] - l[k]);           // 2 * lrarea, :185
-            const double l2 = (fl[k] + fmid[k]) * (mid[k] - l[k]);        // 2 * larea,  :189
-            const double r2 = (fmid[k] + fr[k]) * (r[k] - mid[k]);        // 2 * rarea,  :190
-#endif
             s[k].fmid = fmid[k];
             s[k].area2 = l2 + r2;
             s[k].refine = fabs(s[k].area2 - lr2) > eps2;                  // :191 (strict >)
@@ -165,7 +154,7 @@ __device__ __forceinline__ void pair_step_halves(double ha, double hb, double fa
     hm = 0.5 * m;
     const double mid[2] = {ha + hm, hm + hb};                // :187 for [a, m] and [m, b]
     const double fl[2] = {fa, fm}, fr[2] = {fm, fb};
-    // the parts that do not need F(mid) first (as task_step_k's AQ_EARLY_STEP)
+    // the parts that do not need F(mid) first (as task_step_k's)
     double lr2e[2], wl[2], wr[2];
     lr2e[0] = (fa + fm) * __fma_rn(ha, -2.0, m);             // (fl + fr) * (r - l), :185
     lr2e[1] = (fm + fb) * __fma_rn(hb, 2.0, -m);

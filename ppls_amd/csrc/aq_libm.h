@@ -15,9 +15,6 @@
 // The 2 KiB exp table lives in LDS (one ds_read_b128 per lookup); kernels stage it at entry
 // with aq_stage_exp_table().
 #pragma once
-#ifndef AQ_T2
-#define AQ_T2 0   // measured r02: 30.33 -> 30.49 ms per 8192-integral launch (longer dependency chain): off
-#endif
 #ifndef AQ_PIN_CONSTS
 #define AQ_PIN_CONSTS 1
 #endif
@@ -326,7 +323,7 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
 // FMA). A persistent kernel pins them in VGPRs once (pinned_exp_consts); the default instance lets
 // the compiler choose.
 struct ExpConsts {
-    double shift = kShift + (AQ_T2 ? 128.0 : 0.0), c4 = kC4, c2 = kC2;   // (AQ_T2: see cosh_main_k)
+    double shift = kShift, c4 = kC4, c2 = kC2;
     double inv = kInvLn2N, hi = kNegLn2hiN, lo = kNegLn2loN, c5 = kC5, c3 = kC3;
 };
 __device__ __forceinline__ ExpConsts pinned_exp_consts() {
@@ -345,15 +342,6 @@ __device__ __forceinline__ bool cosh_main_range(double x) {
     const uint32_t ix = hi_word(x) & 0x7fffffffu;
     return ix >= 0x3fd62e43u && ix < 0x40360000u;
 }
-//
-// AQ_T2 (off by default, measured 0.5 % slower): the chains carry t2 = 2 * exp(|x|) instead of t. Rounding commutes with the exact
-// factor 2 in this range, so t2 = RN(2 scale * tmp + 2 scale) = 2 t, and
-//   RN(0.5 / t) = y3, the third Newton iterate of 1 / t2 from rcp(t2) (the compiler's quotient
-//   correction r = fma(-t, q, 0.5), fma(r, y, q) with q = 0.5 y is that step scaled by 2), and
-//   cosh = RN(0.5 t + RN(0.5 / t)) = fma(t2, 0.25, y3),
-// one multiply (q = 0.5 y) fewer per evaluation, bit for bit the same value. The doubled scale costs
-// nothing: with Shift + 128 in place of Shift, ki grows by 128 (index ki & 127 unchanged; the
-// subtraction kd - Shift unchanged) and (ki << 13) adds exactly 2^20 to the scale's high word.
 //
 // TWICE: c[k] = 2 cosh(x[k]) = RN(t + y3), exactly twice glibc's value. With q = 0.5 y2 (exact) the
 // quotient correction's residual fma(-t, q, 0.5) is half the Newton residual e = fma(-t, y2, 1), so
@@ -375,12 +363,6 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
         e[k] = tab[ki[k] & 127];
         if (CHECK) out |= !cosh_main_range(x[k]);
     }
-#if defined(AQ_SETPRIO) && AQ_SETPRIO == 4
-    asm volatile("s_setprio 0" ::: "memory");   // (k_stream priority experiment: the table reads are out)
-#endif
-#if defined(AQ_SETPRIO) && AQ_SETPRIO == 10
-    asm volatile("s_setprio 2");                // (k_stream priority experiment: the chain's second half)
-#endif
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         kd[k] = kd[k] - kk.shift;
@@ -402,33 +384,12 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
         t[k] = __fma_rn(scale, tmp[k], scale);
     }
     double y[K], q[K];
-#if AQ_T2
-    // t[k] holds 2 exp(|x|) here (kk.shift is Shift + 128, see above)
 #pragma unroll
     for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
 #pragma unroll
-    for (int it = 0; it < 3; ++it) {
+    for (int it = 0; it < 2; ++it) {   // two Newton steps (one is not provably enough)
 #pragma unroll
         for (int k = 0; k < K; ++k) y[k] = __fma_rn(y[k], __fma_rn(-t[k], y[k], 1.0), y[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) c[k] = __fma_rn(t[k], 0.25, y[k]);   // 0.5*t + RN(0.5/t)
-    (void)q;
-    return out;
-#endif
-#pragma unroll
-    for (int k = 0; k < K; ++k) y[k] = __builtin_amdgcn_rcp(t[k]);
-#pragma unroll
-    for (int it = 0; it < (AQ_RCP_NEWTON == 3 ? 0 : AQ_RCP_NEWTON); ++it) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) y[k] = __fma_rn(y[k], __fma_rn(-t[k], y[k], 1.0), y[k]);
-    }
-    if (AQ_RCP_NEWTON == 3) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const double e = __fma_rn(-t[k], y[k], 1.0);
-            y[k] = __fma_rn(y[k], __fma_rn(e, e, e), y[k]);
-        }
     }
     if constexpr (TWICE) {
 #pragma unroll

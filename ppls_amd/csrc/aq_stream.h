@@ -136,21 +136,6 @@ constexpr int TAG_SHIFT = 16;
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
-#ifndef AQ_LONE_BLOCK
-#define AQ_LONE_BLOCK 0   // lone launches: contiguous blocks of 2^s seed positions per share (0: snake)
-#endif
-#ifndef AQ_EARLY_FLUSH
-#define AQ_EARLY_FLUSH 0
-#endif
-#ifndef AQ_LONE_GIVE
-#define AQ_LONE_GIVE 0       // give rounds of the per-CU instance (0: as the rest)
-#endif
-#ifndef AQ_LONE_POLL
-#define AQ_LONE_POLL 64
-#endif
-#ifndef AQ_LONE_GIVE_MIN
-#define AQ_LONE_GIVE_MIN 32
-#endif
 #ifndef AQ_LONE_GSPLIT
 #define AQ_LONE_GSPLIT 1   // waves per share in launches of < 16 unsharded integrals (host side, aq_abi.inc)
 #endif
@@ -176,92 +161,34 @@ constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetche
 // land when the ring is down to <= PF_BELOW (a ring simulator of the bench's jobs, tools/ring_sim.py:
 // 80 % of the prefetches then have >= 2 rounds to arrive instead of 1). A ring that overflows while
 // they are in flight cancels them (the pairs are still in the cellar: only ctop moved) and spills.
-#ifndef AQ_PF_LAZY
-#define AQ_PF_LAZY 1
-#endif
 #ifndef AQ_PF_ISSUE
 #define AQ_PF_ISSUE 160   // r03 A/B (8192 x eps=1e-10): 96 -0.6 %, 128 -1.8 %, 160 -2.4 % vs landing after one round
 #endif
-constexpr bool PF_LAZY = AQ_PF_LAZY != 0;
-#ifndef AQ_OUTER_UNI
-#define AQ_OUTER_UNI 1
-#endif
-constexpr bool OUTER_UNI = AQ_OUTER_UNI != 0;
+constexpr int PF_ISSUE = AQ_PF_ISSUE;
+static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
 // In-burst cellar moves (r03): a round that leaves the burst's size window at a cellar edge -- above
 // the spill line, or down to the prefetch issue / landing line -- moves the chunk inside the burst
 // and the burst goes on, where round 2 left the burst for the outer loop (~60 VALU and ~70 SALU of
 // re-checks and state moves per exit, 0.24 exits per round: tools/ring_sim.py, PMC r03e).
-#ifndef AQ_PREBURST_WAIT
-#define AQ_PREBURST_WAIT 0   // r03 A/B: no effect
-#endif
-#ifndef AQ_INB_MASK
-#define AQ_INB_MASK 7
-#endif
-#ifndef AQ_INBURST
-#define AQ_INBURST 1
-#endif
-constexpr bool INBURST = AQ_INBURST != 0;   // re-assert the outer loop's wave state uniform (k_stream)
-#ifndef AQ_PUSH_NOBR
-#define AQ_PUSH_NOBR 1
-#endif
-constexpr bool PUSH_NOBR = AQ_PUSH_NOBR != 0;   // a round's two pushes without branches (lds_push6x2)
-#ifndef AQ_PRO_OVERLAP
-#define AQ_PRO_OVERLAP 1   // the prologue's exp-table loads overlap the rings' set-up (k_stream)
-#endif
-// Wave priority experiments (s_setprio, r03): 1 = a round's start (pop, midpoints, table reads)
-// at priority 3, from the end of its F chains on 0; 2 = a round's end (ballots, pushes, loop
-// control) at 2; 3 = only the pop at 3; 4 = 3 until the exp-table reads are issued (aq_libm.h hook);
-// 5 = as 1 at priority 2; 6 = as 1, dropping to 1
-// 7 = 3 from the pop to the end of the pushes; 8 = the whole burst at 3 (its outer loop at 0);
-// 9 = a fixed priority per wave (wave index mod 3); 10 = as 1, stepping down to 2 once the exp-table
-// reads are written (no memory clobber: only a hint where they issue).
-// r03 A/B (profiles/r03s, r03t): 1, 5, 6 -0.8 %; 3 -0.1 %; 4 +1.0 %; 2 +2.6 %.
-#ifndef AQ_SETPRIO
-#define AQ_SETPRIO 1
-#endif
-#ifndef AQ_SEEDPRIO
-#define AQ_SEEDPRIO 0   // a job's seeding at priority 3 (the experiment beside AQ_SETPRIO)
-#endif
-#ifndef AQ_ONE_WINDOW
-#define AQ_ONE_WINDOW 0   // r03 A/B (profiles/r03q/ab.txt): 2 SALU fewer per round, 0.6 % SLOWER -- off
-#endif
+//
+// Wave priority (r03, profiles/r03s-r03u): each round runs at s_setprio 3 from its pop to the end of
+// its two F chains and at 0 for its tail (ballots, exec windows, pushes, loop control) and everything
+// outside the rounds. The three waves of a SIMD are usually in different phases; the priority lets
+// the one in its latency-bound chain issue ahead of a sibling's SALU-heavy tail.
+//
 // Depth cap checked once per burst (r03): a round pushes every refining task's children and keeps, per
 // lane, the deepest REFINING pair it saw (masked max, as before over the popped pairs); the burst's
 // end tests that against max_depth - 1 -- one compare per burst instead of a compare, two SALU and a
-// branch per round. A burst runs at most give_rounds (<= 32) rounds, so pairs past the cap are at
-// most 32 levels deeper (max_depth <= 127: the depth byte cannot overflow), and a wave that finds the
-// cap exceeded drops its ring and cellar before anything else can see them: nothing deeper than the
-// cap ever reaches the pool or the HBM queue. The run is then invalid (ERRB_DEPTH), as before.
-#ifndef AQ_BURST_CAP
-#define AQ_BURST_CAP 1
-#endif
-#ifndef AQ_LOOPCTL
-#define AQ_LOOPCTL 1
-#endif
-constexpr bool LOOPCTL = AQ_LOOPCTL != 0;
-// Full rounds (r03): while the ring holds >= 64 pairs a round pops 64 and every lane is active, so its
-// masks need no active-lane ballot or AND, its pair count no min and its task count no add (counted
-// per run of full rounds); the round is compiled twice, and the burst runs full rounds in an inner
-// loop whose window keeps the ring at >= 64 pairs.
-#ifndef AQ_FULLR
-#define AQ_FULLR 0   // r03 A/B (profiles/r03q/ab.txt): 7 instructions fewer per full round, 0.9 % SLOWER -- off
-#endif
-constexpr bool FULLR = AQ_FULLR != 0;
-template <bool B>
-struct BoolC {
-    static constexpr bool value = B;
-};   // the burst's edge test on an opaque copy of the round count
-constexpr int PF_ISSUE = PF_LAZY ? AQ_PF_ISSUE : AQ_PF_BELOW;
-static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
-#ifndef AQ_PREFETCH
-#define AQ_PREFETCH 1
-#endif
-constexpr bool PREFETCH = AQ_PREFETCH != 0;   // register-staged cellar prefetch (13 VGPRs)
-#ifndef AQ_SPILL
-#define AQ_SPILL 64   // r02 A/B: 128 at once 4.0 % slower at eps 1e-10, 6.5 % at 1e-12 (more refills)
-#endif
-constexpr int SPILL = AQ_SPILL;   // pairs a ring above WCAP - 64 moves to its cellar at once (a multiple of 64)
-static_assert(SPILL % 64 == 0 && SPILL <= WCAP - 128, "spill whole lanes' worth, keep 64 pairs in the ring");
+// branch per round. A burst runs at most give_rounds rounds, so pairs past the cap are at most
+// give_rounds levels deeper: the depth byte (dt's low 8 bits) cannot carry into SPAN_BIT while
+// (AQ_MAX_LEVELS - 1) + give_rounds < 256 (asserted below). A wave that finds the cap exceeded drops
+// its ring and cellar before anything else can see them: nothing deeper than the cap ever reaches the
+// pool or the HBM queue. The run is then invalid (ERRB_DEPTH), as before. (The histogram instance
+// keeps the per-round test.)
+static_assert((AQ_MAX_LEVELS - 1) + (GIVE_ROUNDS > SKEWED_GIVE ? GIVE_ROUNDS : SKEWED_GIVE) < 256,
+              "a burst's pairs past the depth cap must not carry the depth byte into SPAN_BIT");
+constexpr int SPILL = 64;   // pairs a ring above WCAP - 64 moves to its cellar at once (r02 A/B: 128 at once
+                            // 4.0 % slower at eps 1e-10, 6.5 % at 1e-12: more refills)
 
 struct alignas(128) Line {
     unsigned v;
@@ -413,8 +340,6 @@ struct StreamParams {
     double2 kbounds[PCU_MAXK];      // per-CU launches: the bounds again, as kernel arguments (a scalar load
                                     // with the launch's other arguments, not a cold HBM line at seeding)
     int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
-    int block_s;                    // > 0: share sh seeds the 2^block_s contiguous positions [sh << s, ..)
-                                    // (lone launches, AQ_LONE_BLOCK); 0: the snake partition
 };
 
 // Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
@@ -499,7 +424,7 @@ struct Acc {
     unsigned tasks, leaves, maxd;   // per lane (seeding, mixed rounds)
     unsigned ut, ul;                // wave-uniform task / accepted counts (the rounds' fast path)
     unsigned maxdt;                 // per lane: the deepest pair depth (dt's low byte) a round popped, or
-                                    // with the per-burst cap (AQ_BURST_CAP) the deepest pair a round pushed
+                                    // with the per-burst depth cap the deepest pair a round pushed
     double r = 0.0;                 // per lane: the rounds' accepted areas of the current burst, a plain
                                     // double (one masked add per accepted task), folded into hi / lo
                                     // exactly at every burst's end -- so a lane's rounding error is that of
@@ -557,10 +482,6 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
 
 // {a, b} of integral p through the scalar data cache (a READ: s_load; the host wrote the bounds before
 // the launch and the scalar cache starts every kernel invalidated). p is wave-uniform.
-#ifndef AQ_SLOAD_BOUNDS
-#define AQ_SLOAD_BOUNDS 1
-#endif
-constexpr bool SLOAD_BOUNDS = AQ_SLOAD_BOUNDS != 0;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double2 sload_bounds(const double2* base, int p) {
     const unsigned long long a64 = (unsigned long long)(base + p);
@@ -576,34 +497,8 @@ __device__ __forceinline__ double2 sload_bounds(const double2* base, int p) {
 // field). The pop waits for its own reads (lgkmcnt(0)) inside the asm -- the compiler cannot count
 // LDS operations it does not see -- and the "memory" clobbers keep the compiler's own LDS accesses
 // on their side of both.
-static_assert(LREC * 8 == 50 * 512, "lds_pop6 / lds_push6 assume 50 x 512 B per field");
-// AQ_POP_NOMEM: the round's pop without the "memory" clobber (it is volatile, so it stays ordered with
-// the pushes and cellar moves, all volatile asm; the compiler's own LDS accesses in a burst are reads
-// of the exp table, never written there) -- the clobber made the compiler wait for every LDS access
-// in flight before each pop
-#ifndef AQ_POP_NOMEM
-#define AQ_POP_NOMEM 0
-#endif
-__device__ __forceinline__ void lds_pop6(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
-                                         unsigned& dt) {
-    f64x2 ab, ff, fd;
-    asm volatile(
-        "ds_read2st64_b64 %0, %3 offset1:50\n\t"
-        "ds_read2st64_b64 %1, %3 offset0:100 offset1:150\n\t"
-        "ds_read2st64_b64 %2, %3 offset0:200 offset1:250\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(ab), "=&v"(ff), "=&v"(fd)
-        : "v"(addr)
-#if AQ_POP_NOMEM
-        );
-#else
-        : "memory");
-#endif
-    a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
-    dt = (unsigned)__double_as_longlong(fd.y);
-}
-// ... returning the pair word as the raw 8-byte field (its high half is zero): the round pushes
-// word + 1 (one 64-bit add) with no separate zero for the high half
+static_assert(LREC * 8 == 50 * 512, "lds_pop6w / lds_push6x2 assume 50 x 512 B per field");
+// The pair word comes back as the raw 8-byte field (dt in its low half).
 __device__ __forceinline__ void lds_pop6w(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
                                           unsigned long long& dtw) {
     f64x2 ab, ff, fd;
@@ -617,17 +512,6 @@ __device__ __forceinline__ void lds_pop6w(unsigned addr, double& a, double& b, d
         : "memory");
     a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
     dtw = (unsigned long long)__double_as_longlong(fd.y);
-}
-__device__ __forceinline__ void lds_push6(unsigned addr, double a, double b, double fa, double fm, double fb,
-                                          unsigned dt) {
-    const double dw = __longlong_as_double((long long)dt);
-    asm volatile(
-        "ds_write2st64_b64 %0, %1, %2 offset1:50\n\t"
-        "ds_write2st64_b64 %0, %3, %4 offset0:100 offset1:150\n\t"
-        "ds_write2st64_b64 %0, %5, %6 offset0:200 offset1:250"
-        :
-        : "v"(addr), "v"(a), "v"(b), "v"(fa), "v"(fm), "v"(fb), "v"(dw)
-        : "memory");
 }
 // A round's two pushes (the children pairs of the refining tasks 0 / 1) under the exec masks m0 / m1,
 // with no branch: exec is saved once, set to each mask around its three writes and restored (an empty
@@ -654,68 +538,10 @@ __device__ __forceinline__ void lds_push6x2(unsigned long long m0, unsigned a0, 
           "v"(u1), "v"(v1), "v"(w1), "v"(dw)
         : "memory");
 }
-// masked_acc3 and lds_push6x2 in ONE exec window (AQ_ONE_WINDOW): exec saved once and restored once
-// for the round's two masked area adds, its masked depth max and its two pushes (two SALU fewer).
-// EXEC_FULL: the caller's exec is all 64 lanes (a full round), restored as -1 with nothing saved.
-template <bool EXEC_FULL = false>
-__device__ __forceinline__ void acc3_push6x2(double& hi, double ar0, unsigned long long l0m, double ar1,
-                                             unsigned long long l1m, unsigned& mx, unsigned v, unsigned long long mm,
-                                             unsigned long long m0, unsigned a0, double x0, double y0, double u0,
-                                             double v0, double w0, unsigned long long m1, unsigned a1, double x1,
-                                             double y1, double u1, double v1, double w1, unsigned long long dtw) {
-    const double dw = __longlong_as_double((long long)dtw);
-    unsigned long long saved = 0;
-    if constexpr (EXEC_FULL) {
-        asm volatile(
-            "s_mov_b64 exec, %5\n\t"
-            "v_add_f64 %0, %0, %2\n\t"
-            "s_mov_b64 exec, %6\n\t"
-            "v_add_f64 %0, %0, %3\n\t"
-            "s_mov_b64 exec, %7\n\t"
-            "v_max_u32_sdwa %1, %1, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
-            "s_mov_b64 exec, %8\n\t"
-            "ds_write2st64_b64 %10, %12, %13 offset1:50\n\t"
-            "ds_write2st64_b64 %10, %14, %15 offset0:100 offset1:150\n\t"
-            "ds_write2st64_b64 %10, %16, %22 offset0:200 offset1:250\n\t"
-            "s_mov_b64 exec, %9\n\t"
-            "ds_write2st64_b64 %11, %17, %18 offset1:50\n\t"
-            "ds_write2st64_b64 %11, %19, %20 offset0:100 offset1:150\n\t"
-            "ds_write2st64_b64 %11, %21, %22 offset0:200 offset1:250\n\t"
-            "s_mov_b64 exec, -1"
-            : "+v"(hi), "+v"(mx)
-            : "v"(ar0), "v"(ar1), "v"(v), "s"(l0m), "s"(l1m), "s"(mm), "s"(m0), "s"(m1), "v"(a0), "v"(a1), "v"(x0),
-              "v"(y0), "v"(u0), "v"(v0), "v"(w0), "v"(x1), "v"(y1), "v"(u1), "v"(v1), "v"(w1), "v"(dw)
-            : "memory");
-        return;
-    }
-    asm volatile(
-        "s_mov_b64 %2, exec\n\t"
-        "s_mov_b64 exec, %6\n\t"
-        "v_add_f64 %0, %0, %3\n\t"
-        "s_mov_b64 exec, %7\n\t"
-        "v_add_f64 %0, %0, %4\n\t"
-        "s_mov_b64 exec, %8\n\t"
-        "v_max_u32_sdwa %1, %1, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0\n\t"
-        "s_mov_b64 exec, %9\n\t"
-        "ds_write2st64_b64 %11, %13, %14 offset1:50\n\t"
-        "ds_write2st64_b64 %11, %15, %16 offset0:100 offset1:150\n\t"
-        "ds_write2st64_b64 %11, %17, %23 offset0:200 offset1:250\n\t"
-        "s_mov_b64 exec, %10\n\t"
-        "ds_write2st64_b64 %12, %18, %19 offset1:50\n\t"
-        "ds_write2st64_b64 %12, %20, %21 offset0:100 offset1:150\n\t"
-        "ds_write2st64_b64 %12, %22, %23 offset0:200 offset1:250\n\t"
-        "s_mov_b64 exec, %2"
-        : "+v"(hi), "+v"(mx), "=&s"(saved)
-        : "v"(ar0), "v"(ar1), "v"(v), "s"(l0m), "s"(l1m), "s"(mm), "s"(m0), "s"(m1), "v"(a0), "v"(a1), "v"(x0),
-          "v"(y0), "v"(u0), "v"(v0), "v"(w0), "v"(x1), "v"(y1), "v"(u1), "v"(v1), "v"(w1), "v"(dw)
-        : "memory");
-}
-// The pipelined burst's pair registers: one slot's six fields as lds_pop6 reads them, in two steps.
-// lds_issue6 only ISSUES the three ds_read2st64_b64; lds_wait6 waits for every outstanding LDS access
-// and is the point from which the registers hold the pair -- nothing may read them before (the
-// hardware does not interlock a register an LDS load is still writing). The caller calls lds_wait6
-// late in the same round, after the compiler's own waits for the exp-table reads issued after these
-// loads: LDS accesses of one wave complete in order, so by then the wait costs nothing.
+// One slot's six fields in registers (cellar moves): lds_issue6 only ISSUES the three
+// ds_read2st64_b64; lds_wait6 waits for every outstanding LDS access and is the point from which the
+// registers hold the pair -- nothing may read them before (the hardware does not interlock a register
+// an LDS load is still writing).
 struct PairRegs {
     f64x2 ab, ff, fd;   // {a, b}, {fa, fm}, {fb, dt word}
 };
@@ -796,7 +622,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned pr_base = (unsigned)(uintptr_t)s_pr;   // LDS byte offset of the pair block (low word of its flat address)
     const unsigned long long t_entry = DIAG ? rtc() : 0ull;
-#if AQ_PRO_OVERLAP
     // the exp table's global loads go out first and land in LDS after the other set-up stores (the
     // rings' harmless pairs among them): their latency, a cold HBM read at every launch, overlaps
     // the set-up instead of preceding it
@@ -812,9 +637,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
         }
     }
-#else
-    stage_f_table<FID>(tab, P.gtab);
-#endif
     if (bid == 0)
         for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
     if (tid == 0) {
@@ -827,14 +649,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
-#if AQ_PRO_OVERLAP
     if (FID == F_SIN_RECIP) {
         if (tid < (unsigned)AQ_SINCOS_TAB_N) reinterpret_cast<double*>(tab)[tid] = sv;
     } else if (tid < 128u) {
         tab[tid].tail_bits = tv.tail_bits;
         tab[tid].sbits = tv.sbits;
     }
-#endif
     __syncthreads();   // the only workgroup barrier before the exit
     if constexpr (DIAG) { if (tid == 0) s_dg[DG_T_INIT] = rtc(); }
 
@@ -875,13 +695,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     asm volatile("" : "+v"(ring_vmask));   // kept in a VGPR (see ring_addr)
 
     Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u, 0u};
-    // every ring slot holds a harmless pair from the start: rounds read all 64 lanes' slots
-    if constexpr (!AQ_PRO_OVERLAP) {
-        for (unsigned i = lane; i < (unsigned)WCAP; i += 64) {
-            const unsigned j = base + i;
-            s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
-        }
-    }
+    // (every ring slot holds a harmless pair from the start -- the prologue: rounds read all 64 lanes' slots)
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
     Cellar* __restrict__ cel = P.cellar + w_all;
@@ -909,13 +723,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // sin(1/x) (config 4) piles nearly all of its tree into one small region: its waves look for idle
     // siblings every SKEWED_GIVE rounds (a lone integral 79 -> 70 us at 4; cosh4 keeps 32, where 4 cost
     // the eps=1e-12 lone tree 47 -> 61 us and the bench 0.6 %; profiles/r02_ab/fast_give_poll*.txt)
-    // (the per-CU instance -- launches of a few integrals -- may use its own cadence, AQ_LONE_GIVE*)
-    constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE
-                                     : (PCU && AQ_LONE_GIVE > 0) ? (unsigned)AQ_LONE_GIVE : (unsigned)GIVE_ROUNDS;
-    constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL
-                                     : (PCU && AQ_LONE_GIVE > 0) ? (unsigned)AQ_LONE_POLL : (unsigned)POLL_ROUNDS;
-    constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN
-                                  : (PCU && AQ_LONE_GIVE > 0) ? (unsigned)AQ_LONE_GIVE_MIN : (unsigned)GIVE_MIN;
+    // (a faster cadence for lone launches, give every 4 / 8 rounds: slower, profiles/r03zb)
+    constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE : (unsigned)GIVE_ROUNDS;
+    constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL : (unsigned)POLL_ROUNDS;
+    constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN : (unsigned)GIVE_MIN;
     unsigned poll_ctr = wid * (poll_rounds / NW);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
@@ -941,30 +752,19 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
     };
     const ExpConsts kk = pinned_exp_consts();
-    // AQ_SETPRIO 9: a fixed priority per wave (0 / 1 / 2 by wave index mod 3: one wave per SIMD runs
-    // ahead of its two siblings)
-    if constexpr (AQ_SETPRIO == 9) {
-        const unsigned pr = wid % 3u;
-        if (pr == 1u) asm volatile("s_setprio 1");
-        else if (pr == 2u) asm volatile("s_setprio 2");
-    }
-    // the depth cap per burst (AQ_BURST_CAP); the histogram instance keeps the per-round test
-    constexpr bool burst_cap = AQ_BURST_CAP != 0 && !HIST;
-    // the round's accumulations and pushes in one exec window (not in the histogram / diagnostic
-    // instances, whose per-round extras sit between them)
-    constexpr bool one_window = AQ_ONE_WINDOW != 0 && PUSH_NOBR && !HIST && !DIAG;
+    // the depth cap per burst (see the file's configuration notes); the histogram instance keeps the
+    // per-round test
+    constexpr bool burst_cap = !HIST;
     for (;;) {
         // the wave's ring / cellar state, re-asserted uniform once per iteration: the loop's many
         // divergent lane-level blocks (copies, seeding) otherwise leave it in VGPRs, and every check
         // below becomes a v_cmp + exec-mask branch instead of a scalar compare
-        if constexpr (OUTER_UNI) {
-            top = uni(top);
-            bot = uni(bot);
-            ctop = uni(ctop);
-            pf_n = uni(pf_n);
-            poll_ctr = uni(poll_ctr);
-        }
-        if (pf_n && (!PF_LAZY || top - bot <= (unsigned)PF_BELOW)) {
+        top = uni(top);
+        bot = uni(bot);
+        ctop = uni(ctop);
+        pf_n = uni(pf_n);
+        poll_ctr = uni(poll_ctr);
+        if (pf_n && top - bot <= (unsigned)PF_BELOW) {
             if (bot < 64u) {   // keep ring indices non-negative (slots are index % WCAP)
                 bot += (unsigned)WCAP;
                 top += (unsigned)WCAP;
@@ -1027,11 +827,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (fresh && job < total_jobs) {
                 seed = true;
             } else {
-                // per-CU launches (a few integrals): a wave with nothing left to seed flushes its
-                // accumulators before it looks for pool work or goes idle -- while other waves still
-                // run, instead of every wave flushing at once after the run's end (AQ_EARLY_FLUSH)
-                if constexpr (PCU && AQ_EARLY_FLUSH)
-                    if (!counted_idle && job >= total_jobs) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
                 wave_lock(&S.lock, lane, lock_spins);
                 {
                     const unsigned avail = uni(S.ptop - S.pbot);
@@ -1096,7 +891,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
             if (seed) {
                 // ---- wave-local seeding of job `job` (see the file header)
-                if constexpr (AQ_SEEDPRIO) asm volatile("s_setprio 3");
                 unsigned long long cs = 0;
                 if constexpr (DIAG) {
                     cs = clk();
@@ -1135,7 +929,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // once per job. A scalar load (lgkmcnt), so the wait for it does not also wait for the
                 // previous integral's flush atomics and this job's claim (vmcnt, in issue order), which
                 // stay in flight while the job seeds (C3 eps=1e-3 A/B: profiles/r02_ab/sload_bounds.txt)
-                const double2 ab = PCU ? P.kbounds[p] : (SLOAD_BOUNDS ? sload_bounds(P.bounds, p) : P.bounds[p]);
+                const double2 ab = PCU ? P.kbounds[p] : sload_bounds(P.bounds, p);
                 if (static_jobs) {
                     // launches of few integrals cut every integral into one share per wave: wave w seeds share w of
                     // each integral in turn (static stride, no claim). 3072 waves claiming through one
@@ -1168,81 +962,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 unsigned long long cp1 = 0, cp2 = 0;
                 bool alive = false;
                 double l = A, r = B, fl = 0.0, fr = 0.0, mid = 0.0, fmid = 0.0;
-                if (P.block_s > 0) {
-                    // contiguous blocks (lone launches, AQ_LONE_BLOCK): share sh owns the 2^s positions
-                    // [sh << s, (sh + 1) << s) at depth D = Dp + s, so its nodes are the path of its block
-                    // root (depths 0..Dp-1: lane d) and the block's whole subtree (depth Dp + e, index
-                    // t < 2^e: lane Dp + 2^e - 1 + t) -- each surviving wave starts with up to 2^s pairs
-                    // where the snake deal's 3 positions gave it ~3 (a lone tree's rounds were half
-                    // empty for their first five). A path node is owned by the share whose block starts
-                    // at its leftmost position, a subtree node by its block's share: every node at depth
-                    // <= D is counted once, as in the snake partition.
-                    const unsigned sb = (unsigned)P.block_s;
-                    const unsigned Dp = (unsigned)D - sb;
-                    const unsigned nn = Dp + (2u << sb) - 1u;   // + F(A), F(B): <= 64 (host-checked)
-                    const unsigned q = lane;
-                    const bool isnode = q < nn;
-                    unsigned d = 0;
-                    unsigned long long g = 0;   // the node's index at its depth
-                    if (isnode) {
-                        if (q < Dp) {
-                            d = q;
-                            g = (unsigned long long)sh >> (Dp - d);
-                        } else {
-                            const unsigned u = q - Dp, e = 31u - (unsigned)__builtin_clz(u + 1u);
-                            d = Dp + e;
-                            g = ((unsigned long long)sh << e) + (u - ((1u << e) - 1u));
-                        }
-                    }
-                    // the lane of this node's ancestor at depth i < d
-                    auto lane_of = [&](unsigned i) -> unsigned {
-                        const unsigned long long gi = g >> (d - i);
-                        if (i < Dp) return i;
-                        const unsigned e = i - Dp;
-                        return Dp + ((1u << e) - 1u) + (unsigned)(gi - ((unsigned long long)sh << e));
-                    };
-                    unsigned li = nn, ri = nn + 1u;
-                    unsigned long long ancm = 0;   // the ancestors' lanes
-                    for (unsigned i = 0; i < d; ++i) {
-                        const double mm = (l + r) / 2;
-                        const unsigned la = lane_of(i);
-                        ancm |= 1ull << la;
-                        if ((g >> (d - 1u - i)) & 1ull) { l = mm; li = la; } else { r = mm; ri = la; }
-                    }
-                    mid = (l + r) / 2;                                        // :187
-                    if (q < nn + 2u) {
-                        fmid = integrand<FID>(isnode ? mid : (q == nn ? A : B), tab);   // :188
-                        fm[q] = fmid;
-                    }
-                    bool refine = false;
-                    double leafarea = 0.0;
-                    if (isnode) {
-                        fl = fm[li];
-                        fr = fm[ri];
-                        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
-                        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
-                        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
-                        refine = fabs((larea + rarea) - lrarea) > eps;       // :191
-                        leafarea = larea + rarea;                             // :199
-                    }
-                    const unsigned long long leafm = __ballot(isnode && !refine);
-                    const bool reach = isnode && (leafm & ancm) == 0ull;     // no leaf above it: it exists
-                    const bool owned = d >= Dp || (sh & ((1u << (Dp - d)) - 1u)) == 0u;
-                    if (reach && owned) {
-                        ++acc.tasks;
-                        acc.maxd = max(acc.maxd, d + 1u);
-                        if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
-                        if (!refine) {
-                            dd_add(acc.hi, acc.lo, leafarea / area_scale<FID>());   // :199 -> :149 (doubled, exact)
-                            ++acc.leaves;
-                            if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
-                        } else if ((int)d + 1 >= max_depth) {
-                            err |= ERRB_DEPTH;
-                        }
-                    }
-                    alive = reach && refine && d == (unsigned)D && D + 1 < max_depth;
-                    if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
-                } else if (nnodes <= 64) {
+                if (nnodes <= 64) {
                     // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
                     // decision; the first leaf depth of every position comes from ONE ballot
                     unsigned long long ca = 0, cb = 0;
@@ -1414,7 +1134,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         atomicMax(&s_dg[DG_T_SEEDED], rtc());
                     }
                 }
-                if constexpr (AQ_SEEDPRIO) asm volatile("s_setprio 0");
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
@@ -1525,7 +1244,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // ---- keep the ring from overflowing: its bottom 64 pairs go to the cellar, else the pool,
         //      else an HBM chunk
         if (size > (unsigned)(WCAP - 64)) {
-            if (PF_LAZY && pf_n) {
+            if (pf_n) {
                 // a prefetch in flight is cancelled: its pairs never left the cellar (the loads land in
                 // registers nobody reads; the next spill writes above them)
                 ctop += pf_n;
@@ -1641,7 +1360,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
 
         // ---- running low: fetch the next 64 cellar pairs now, land them next iteration
-        if (PREFETCH && ctop > 0 && pf_n == 0 && size <= (unsigned)PF_ISSUE) {
+        if (ctop > 0 && pf_n == 0 && size <= (unsigned)PF_ISSUE) {
             pf_n = 64u;   // ctop is a whole number of chunks
             ctop -= pf_n;
             // (same-wave, same-address order: no wait for the spills)
@@ -1662,173 +1381,110 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         unsigned b_bot = uni(bot), b_ctop = uni(ctop), b_pf = uni(pf_n);
         bool b_mixed = uni(mixed);
         // the burst goes on while lo < size <= hi and the next round is no give / poll round:
-        // lo = PF_BELOW while the cellar holds pairs to prefetch (else 0: stop when empty), hi =
-        // WCAP - 64 (near overflow), or hi = lo while a prefetch is in flight (one round only).
-        // One subtract and one compare per round, and one compare for the round counter.
+        // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar holds pairs
+        // and none is (issue one), else 0 (stop when empty); hi = WCAP - 64 (near overflow). One
+        // subtract and one compare per round, and one compare for the round counter.
         unsigned b_lo1, b_span;
-        unsigned b_lo1f, b_spanf;   // the full rounds' window: lo raised to 63 (a full round needs 64 pairs)
         auto window = [&]() {
-            if constexpr (PF_LAZY) {
-                // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar
-                // holds pairs and none is (issue one), else 0 (stop when empty); hi = WCAP - 64
-                b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_ISSUE : 0u)) + 1u;
-                b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
-            } else {
-                b_lo1 = ((PREFETCH && b_ctop > 0u) ? (unsigned)PF_BELOW : 0u) + 1u;
-                b_span = b_pf != 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1;
-            }
-            b_lo1f = max(b_lo1, 64u);
-            b_spanf = b_span == 0u ? 0u : (unsigned)(WCAP - 64) + 1u - b_lo1f;
+            b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : (b_ctop > 0u ? (unsigned)PF_ISSUE : 0u)) + 1u;
+            b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
         };
         window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
         unsigned b_rem = b_max;   // rounds left up to the give / poll round (counted down: no copy of a
                                   // round counter per round)
-#if AQ_PREBURST_WAIT
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), compiler-visible: nothing pending at the burst's header
-#endif
-        // one round: FULL = the ring holds >= 64 pairs (every lane pops one)
-        auto round_body = [&](auto full) __attribute__((always_inline)) {
-            constexpr bool FULL = decltype(full)::value;
-                // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
-                //      tasks of a pair are evaluated together (two interleaved cosh chains)
-                unsigned long long c0 = 0, c1 = 0;
-                if constexpr (DIAG) c0 = clk();
-                const unsigned n = FULL ? 64u : min(b_size, 64u);
-                const unsigned b0 = b_top - n;
-                const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
-                // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
-                double pa, pb, pfa, pfm, pfb;
-                unsigned long long dtw;   // the pair word's 8-byte field (dt in its low half)
-                if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 3 || AQ_SETPRIO == 4 || AQ_SETPRIO == 6 ||
-                              AQ_SETPRIO == 7 || AQ_SETPRIO == 10)
-                    asm volatile("s_setprio 3");
-                if constexpr (AQ_SETPRIO == 5) asm volatile("s_setprio 2");
-                if constexpr (AQ_SETPRIO == 2) asm volatile("s_setprio 0");
-                lds_pop6w(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dtw);
-                if constexpr (AQ_SETPRIO == 3) asm volatile("s_setprio 0");
-                const unsigned dt = (unsigned)dtw;
-                Step2 st[2];
-                // both midpoints lie in [pa, pb]: one range test for the pair
-                // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
-                // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
-                // compiler turns the byte test into an and plus a compare
-                unsigned long long nospan = 0ull;
-                if constexpr (FID == F_COSH4)
-                    asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
-                // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
-                // measured 0.9 % slower)
-                // a full round (FULL: 64 pairs or more in the ring) has every lane active: its masks need no
-                // active-lane ballot, and no AND with one
-                const unsigned long long am = FULL ? ~0ull : __ballot(lane < n);
-                // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
-                double pm, hm;
-                pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
-                if constexpr (AQ_SETPRIO == 1 || AQ_SETPRIO == 5 || AQ_SETPRIO == 10) asm volatile("s_setprio 0");
-                if constexpr (AQ_SETPRIO == 6) asm volatile("s_setprio 1");
-                if constexpr (AQ_SETPRIO == 2) asm volatile("s_setprio 2");
-                // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
-                // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
-                // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
-                const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
-                unsigned long long okm = am;
-                if constexpr (!burst_cap) {
-                    const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
-                    okm = am & dm;
-                    // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
-                    const unsigned long long atcap = am & ~dm;
-                    if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
-                }
-                // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
-                // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
-                // counts are wave-level, the area one masked add per accepted task.
-                const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
-                if constexpr (!FULL) b_n += n;   // tasks 2n (full rounds: counted per run of rounds); accepted:
-                                                 // counted once per burst from the ring's growth (below)
-                // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-                // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
-                // with the per-burst depth cap, the deepest refining pair
-                const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-                const unsigned long long cdtw = dtw + 1ull;         // depth + 1, same integral
-                const unsigned cdt = (unsigned)cdtw;
-                if constexpr (!one_window)
-                    masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
-                                burst_cap ? (mask0 | mask1) : am);
-                if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
-                                        // takes and seeds switch the tag); checked in diagnostic builds
-                    const int rtag = (int)(dt >> TAG_SHIFT);
-                    b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
-                }
-                if (HIST) {
-                    const unsigned d = dt & 255u;
-                    if (__builtin_amdgcn_inverse_ballot_w64(am)) {
-                        atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
-                        const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
-                        if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
-                    }
-                }
-                if constexpr (DIAG) c1 = clk();
-                // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
-                // seeded with the round's base slot (the counts start at b0s / b0s + cnt0)
-                const unsigned cnt0 = (unsigned)__popcll(mask0);
-                if constexpr (one_window) {
-                    acc3_push6x2<FULL>(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
-                                 burst_cap ? (mask0 | mask1) : am,
-                                 mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
-                                 mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
-                                 cdtw);
-                } else if constexpr (PUSH_NOBR) {
-                    lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
-                                mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
-                                cdt);
-                } else {
-                    if (__builtin_amdgcn_inverse_ballot_w64(mask0)) {
-                        lds_push6(ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm, cdt);
-                    }
-                    if (__builtin_amdgcn_inverse_ballot_w64(mask1)) {
-                        lds_push6(ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb, cdt);
-                    }
-                }
-                b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
-                if constexpr (AQ_SETPRIO == 7) asm volatile("s_setprio 0");
-                if constexpr (DIAG) {
-                    if (lane == 0) {
-                        const unsigned long long c2 = clk();
-                        atomicAdd(&s_dg[DG_ROUNDS], 1ull);
-                        atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
-                        atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
-                        atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
-                        atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
-                        atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
-                    }
-                    const unsigned nt = 2u * n;
-                    if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
-                }
-        };
-        if constexpr (AQ_SETPRIO == 8) asm volatile("s_setprio 3");
         bool b_go;
-        for (;;) {   // the burst: runs of rounds (the inner loops, their exits one compare each), and the
-                     // cellar moves at the window's edges between them
+        for (;;) {   // the burst: runs of rounds (the inner loop, its exit one compare), and the cellar
+                     // moves at the window's edges between them
         for (;;) {
-            if (FULLR && b_size >= 64u) {
-                // full rounds while the window holds AND the ring keeps >= 64 pairs (lo raised to 64)
-                const unsigned r_in = b_rem;
-                unsigned szf, span_f;
-                do {
-                    --b_rem;   // (first: the old count is dead before the round, so no copy at the latch)
-                    round_body(BoolC<true>{});
-                    szf = b_top - b_bot;
-                    span_f = b_rem != 0u ? b_spanf : 0u;
-                    asm("" : "+s"(span_f));
-                    __builtin_amdgcn_wave_barrier();
-                } while (szf - b_lo1f < span_f);
-                b_n += 64u * (r_in - b_rem);
-                b_size = szf;
-            } else {
-                round_body(BoolC<false>{});
-                b_size = b_top - b_bot;
-                --b_rem;
+            // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
+            //      tasks of a pair are evaluated together (two interleaved cosh chains)
+            unsigned long long c0 = 0, c1 = 0;
+            if constexpr (DIAG) c0 = clk();
+            const unsigned n = min(b_size, 64u);
+            const unsigned b0 = b_top - n;
+            const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
+            // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
+            double pa, pb, pfa, pfm, pfb;
+            unsigned long long dtw;   // the pair word's 8-byte field (dt in its low half)
+            asm volatile("s_setprio 3");   // the pop and the F chains ahead of the siblings' tails
+            lds_pop6w(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dtw);
+            const unsigned dt = (unsigned)dtw;
+            Step2 st[2];
+            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
+            // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
+            // compiler turns the byte test into an and plus a compare
+            unsigned long long nospan = 0ull;
+            if constexpr (FID == F_COSH4)
+                asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
+            // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
+            // measured 0.9 % slower)
+            const unsigned long long am = __ballot(lane < n);
+            // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
+            double pm, hm;
+            pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+            asm volatile("s_setprio 0");
+            // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
+            // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
+            // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
+            const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
+            unsigned long long okm = am;
+            if constexpr (!burst_cap) {
+                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+                okm = am & dm;
+                // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
+                const unsigned long long atcap = am & ~dm;
+                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
             }
+            // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
+            // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
+            // counts are wave-level, the area one masked add per accepted task.
+            const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
+            b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
+            // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
+            // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
+            // with the per-burst depth cap, the deepest refining pair
+            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
+            const unsigned cdt = dt + 1u;   // depth + 1, same integral
+            masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                        burst_cap ? (mask0 | mask1) : am);
+            if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
+                                    // takes and seeds switch the tag); checked in diagnostic builds
+                const int rtag = (int)(dt >> TAG_SHIFT);
+                b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
+            }
+            if (HIST) {
+                const unsigned d = dt & 255u;
+                if (__builtin_amdgcn_inverse_ballot_w64(am)) {
+                    atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                    const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
+                    if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+                }
+            }
+            if constexpr (DIAG) c1 = clk();
+            // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
+            // seeded with the round's base slot (the counts start at b0s / b0s + cnt0); both pushes
+            // under exec masks, no branch (lds_push6x2)
+            const unsigned cnt0 = (unsigned)__popcll(mask0);
+            lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
+                        mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
+                        cdt);
+            b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
+            if constexpr (DIAG) {
+                if (lane == 0) {
+                    const unsigned long long c2 = clk();
+                    atomicAdd(&s_dg[DG_ROUNDS], 1ull);
+                    atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
+                    atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
+                    atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
+                    atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
+                    atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
+                }
+                const unsigned nt = 2u * n;
+                if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
+            }
+            b_size = b_top - b_bot;
+            --b_rem;
             // one compare: the give / poll round closes the size window (opaque, so the compiler does
             // not split it back into two conditions joined by SALU selects)
             unsigned span_r = b_rem != 0u ? b_span : 0u;
@@ -1840,13 +1496,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             // the edge test reads b_rem through an opaque copy: otherwise the compiler keeps `b_rem != 0`
             // as a materialised lane mask across the round's select
             unsigned b_re = b_rem;
-            if constexpr (LOOPCTL) asm volatile("" : "+s"(b_re));
+            asm volatile("" : "+s"(b_re));
             const unsigned sz = b_size;
-            if (INBURST && PF_LAZY && b_re != 0u && sz != 0u) {
+            if (b_re != 0u && sz != 0u) {
                 // a cellar edge (not the give / poll round, not an empty ring): move the chunk here
                 // and go on (the cellar-full spill and the pool / queue fallbacks stay outside)
                 if (sz > (unsigned)(WCAP - 64)) {
-                    if ((AQ_INB_MASK & 1) && b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
+                    if (b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
                         if (b_pf) {   // cancel the prefetch in flight (its pairs never left the cellar)
                             b_ctop += b_pf;
                             b_pf = 0;
@@ -1856,7 +1512,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         b_bot += (unsigned)SPILL;
                         b_go = true;
                     }
-                } else if ((AQ_INB_MASK & 2) && b_pf) {                   // down to PF_BELOW: land the prefetch
+                } else if (b_pf) {                   // down to PF_BELOW: land the prefetch
                     if (b_bot < 64u) {
                         b_bot += (unsigned)WCAP;
                         b_top += (unsigned)WCAP;
@@ -1866,7 +1522,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)b_pf); }
                     b_pf = 0;
                     b_go = true;
-                } else if ((AQ_INB_MASK & 4) && PREFETCH && b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
+                } else if (b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
                     b_pf = 64u;
                     b_ctop -= 64u;
                     pf = chunk_load(&cel->c[b_ctop / 64u], lane);
@@ -1880,7 +1536,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             __builtin_amdgcn_wave_barrier();
             if (!b_go) break;
         }
-        if constexpr (AQ_SETPRIO == 8) asm volatile("s_setprio 0");
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;
@@ -1898,7 +1553,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (burst_cap) {
             // the per-burst depth cap: a pushed pair at depth >= max_depth means a task at the cap
             // refined. The wave drops its ring and cellar (the run is invalid) before anything can hand
-            // the pairs on, so nothing past the cap leaves the wave (see AQ_BURST_CAP)
+            // the pairs on, so nothing past the cap leaves the wave (the configuration notes above)
             if (__builtin_expect(__ballot((acc.maxdt & 255u) >= (unsigned)max_depth) != 0ull, 0)) {
                 err |= ERRB_DEPTH;
                 top = bot;

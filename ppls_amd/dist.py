@@ -168,7 +168,11 @@ class HipBatchRunner:
         if len(a) == 0:
             return np.zeros((0, ROW), np.int64)
         n = len(a)
-        out = torch.empty((n, ROW), dtype=torch.int64, device=torch.device("cuda", self.ctx.device))
+        dev = torch.device("cuda", self.ctx.device)
+        out = torch.empty((n, ROW), dtype=torch.int64, device=dev)
+        # the caching allocator orders `out` on torch's current stream, but the gather below writes it
+        # on the library's own stream: whatever torch work still uses the block must finish first
+        torch.cuda.current_stream(dev).synchronize()
         self.ctx.kernel_timing(True)
         try:
             self.ctx.integrate_mixed_async(a, b, shards, nshards, eps, first_slot=0, integrand=integrand)

@@ -139,6 +139,13 @@ def libm_bits():
     print("libm_bits:", x.size, "points;", tp.size, "distinct-ish tree points at 1e-10")
 
 
+def _batch10_part(rng):
+    s, e = rng
+    a, b = O.batch_bounds(e)
+    _, t, lv = O.integrate_batch(a[s:e], b[s:e], 1e-10)
+    return int(lv.sum()), int(t.sum())
+
+
 def batch():
     a, b = O.batch_bounds(10000)
     ar3, t3, l3 = O.integrate_batch(a, b, 1e-3)
@@ -159,6 +166,16 @@ def batch():
     }
     # SURVEY §8d KAT: the first 10 000 draws give mean leaves 711.5 at eps=1e-3
     assert abs(out["mean_leaves_eps1e-3"] - 711.5) < 0.05, out["mean_leaves_eps1e-3"]
+    # ... and 153 330.8 at eps=1e-10: the exact sums (3e9 tasks; 8 processes, ~1 min), which the
+    # bench's C3 pass checks its first 10 000 integrals against
+    from multiprocessing import Pool
+    with Pool(8) as pool:
+        parts = pool.map(_batch10_part, [(i, min(i + 250, 10000)) for i in range(0, 10000, 250)], chunksize=1)
+    out["kat_n_eps1e-10"] = 10000
+    out["kat_sum_leaves_eps1e-10"] = sum(p[0] for p in parts)
+    out["kat_sum_tasks_eps1e-10"] = sum(p[1] for p in parts)
+    assert round(out["kat_sum_leaves_eps1e-10"] / 10000, 1) == 153330.8, out["kat_sum_leaves_eps1e-10"]
+    assert out["kat_sum_tasks_eps1e-10"] == 2 * out["kat_sum_leaves_eps1e-10"] - 10000
     with open(os.path.join(OUT, "batch.json"), "w") as f:
         json.dump(out, f, indent=1)
     print("batch: mean leaves 1e-3 =", out["mean_leaves_eps1e-3"], "; first", n10, "at 1e-10 mean",

@@ -48,6 +48,7 @@ def test_strerror_and_arg_validation(lib):
     import ctypes
     assert lib.aq_strerror(0) == b"ok"
     assert lib.aq_strerror(-5) == b"maximum refinement depth reached"
+    assert lib.aq_strerror(-9) == b"the persistent grid cannot be co-resident on the device"
     # NULL context / arguments are rejected before any device call
     assert lib.aq_integrate(None, None, None) == -1
     assert lib.aq_fetch(None, 0, None) == -1

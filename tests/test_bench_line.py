@@ -76,3 +76,71 @@ def test_bench_line_single_process():
     assert bench.ranks_seen(dist, "cpu", False) == 1
     st = bench.rank_stats(dist, "cpu", False, 12.5, 2, 100.0, 0.02)
     assert st["kernel_ms"] == [12.5] and st["tasks"] == [100] and st["task_imbalance"] == 1.0
+
+
+def test_launcher_spawns_n_ranks_after_the_cpu_baseline():
+    """--gpus 2 with no launcher: the CPU baseline is timed first (no GPU call in this process), then
+    ONE child torch.distributed.run starts 2 ranks of this same script with the same arguments, the
+    baseline travels to rank 0 through the environment, and the children's status is returned."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    calls, order = [], []
+    args = bench.parse(["--gpus", "2", "--steps", "3", "--warmup", "1"])
+
+    def baseline(eps):
+        order.append("baseline")
+        return {"value": 1.0, "kind": "port", "eps": eps}
+
+    def runner(cmd, env):
+        order.append("runner")
+        calls.append((cmd, env))
+        return 7
+
+    rc = bench.spawn_ranks(args, ["--gpus", "2", "--steps", "3", "--warmup", "1"], runner=runner, baseline=baseline)
+    assert rc == 7 and order == ["baseline", "runner"] and len(calls) == 1
+    cmd, env = calls[0]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--nnodes=1" in cmd and "127.0.0.1" in cmd
+    assert cmd[-7:] == [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
+    assert json.loads(env[bench.CPU_ENV]) == {"value": 1.0, "kind": "port", "eps": 1e-10}
+    # --no-cpu-baseline: nothing timed, nothing handed over
+    calls.clear()
+    order.clear()
+    args = bench.parse(["--gpus", "4", "--no-cpu-baseline"])
+    env0 = dict(os.environ)
+    env0.pop(bench.CPU_ENV, None)
+    rc = bench.spawn_ranks(args, ["--gpus", "4", "--no-cpu-baseline"], runner=runner, baseline=baseline)
+    assert rc == 7 and order == ["runner"] and bench.CPU_ENV not in calls[0][1]
+
+
+def test_launcher_world_size_mismatch_fails():
+    """Under a launcher, WORLD_SIZE != --gpus is an error exit (before any GPU call), not a fallback."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_c3_bounds_and_kat_fixture():
+    """The bench's C3 generator reproduces the committed splitmix64 bounds, and the exact KAT of the
+    first 10 000 draws at eps=1e-10 is consistent (T = 2L - 1 summed, mean leaves 153 330.8)."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, "tests", "golden", "batch.json")) as f:
+        g = json.load(f)
+    a, b = bench.splitmix64_bounds(16)
+    assert [[float(x).hex(), float(y).hex()] for x, y in zip(a, b)] == g["first_bounds_hex"]
+    n = g["kat_n_eps1e-10"]
+    assert n == 10000 and g["kat_sum_tasks_eps1e-10"] == 2 * g["kat_sum_leaves_eps1e-10"] - n
+    assert round(g["kat_sum_leaves_eps1e-10"] / n, 1) == 153330.8
+
+
+def test_area_check():
+    sys.path.insert(0, ROOT)
+    import bench
+    want = bench.GOLDEN[1e-10][2]
+    assert bench.areas_ok([want, want * (1 + 5e-13)], want)
+    assert not bench.areas_ok([want, want * (1 + 2e-12)], want)

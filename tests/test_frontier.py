@@ -226,3 +226,17 @@ def test_rebalanced_frontier_two_ranks_one_gpu(trees, every):
             assert abs(area - float(g["area_quad"])) <= AREA_RTOL * abs(float(g["area_quad"]))
             assert moved > 0
             assert max(per_rank) <= (g["tasks"] / 2 + 64 if every == 1 else 0.75 * g["tasks"])
+
+
+@pytest.mark.gpu
+def test_levels_after_small_frontier_on_one_context(trees):
+    """a small-capacity frontier run leaves smaller buffers in the context; the level path
+    that follows on the same context grows them to its own minimum instead of overflowing."""
+    from ppls_amd import Context, Problem, frontier
+    g = trees["cosh4_eps1e-12"]
+    with Context(0) as ctx:
+        r = frontier.integrate(Problem(0, 0.0, 5.0, 1e-3), stepper=frontier.HipStepper(ctx), capacity=1 << 16)
+        assert (r.tasks, r.accepted) == (6567, 3284)
+        lv = ctx.integrate_levels(Problem(0, 0.0, 5.0, 1e-12))
+        assert (lv.tasks, lv.accepted, lv.levels) == (g["tasks"], g["leaves"], g["levels"])
+        assert lv.tasks_per_level == g["tasks_per_level"]

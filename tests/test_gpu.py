@@ -689,3 +689,39 @@ def test_depth_cap_boundary(ctx, trees, hist):
     finally:
         ctx.set_level_histograms(True)   # the context's default
     assert ctx.integrate(Problem(eps=1e-3)).tasks == 6567
+
+
+def test_grid_that_cannot_be_resident_is_refused(trees, monkeypatch):
+    """the persistent grid's workgroups wait on each other, so a grid larger than the
+    device can hold at once is refused before launch with AQ_ERESIDENT (-9) -- not a 10 s stall. A
+    smaller grid (AQ_GRID) is resident and exact; so is the cooperative launch (AQ_COOP=1)."""
+    from ppls_amd import AquadError, Context, Problem
+    g = trees["cosh4_eps1e-10"]
+    with Context(0) as c0:
+        ncu = c0.num_cus
+    monkeypatch.setenv("AQ_GRID", str(2 * ncu))   # one workgroup per CU is all k_stream's LDS allows
+    c = Context(0)
+    try:
+        with pytest.raises(AquadError) as e:
+            c.integrate(Problem(eps=1e-10))
+        assert e.value.code == -9
+        with pytest.raises(AquadError) as e:
+            c.integrate_many_async(np.zeros(64), np.full(64, 5.0), 1e-10, first_slot=0)
+        assert e.value.code == -9
+    finally:
+        c.close()
+    for env in ({"AQ_GRID": str(ncu // 2)}, {"AQ_GRID": "", "AQ_COOP": "1"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = Context(0)
+        try:
+            r = c.integrate(Problem(eps=1e-10))
+            assert (r.tasks, r.accepted, r.levels) == (g["tasks"], g["leaves"], g["levels"]), env
+            assert _area_ok(r.area, g["area_quad"])
+            c.set_level_histograms(False)
+            c.integrate_many_async(np.zeros(64), np.full(64, 5.0), 1e-10, first_slot=0)
+            for i in (0, 63):
+                r = c.fetch(i)
+                assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"]), env
+        finally:
+            c.close()

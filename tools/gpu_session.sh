@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session of several measurements, each under its own time limit; a failing step ends the
 # script (no later GPU step runs after a fault). Output under gpurun_out/<tag>/.
-#   tools/gpu_session.sh <tag> [steps...]   steps: tests ubench ab front bench12 bench lone diag smoke
+#   tools/gpu_session.sh <tag> [steps...]   steps: tests ubench ab front bench12 bench lone lonecoop shared2 diag smoke ...
 #   (AB_GLOB_K / AB_GLOB_F: the library variants the k_stream / frontier A/Bs take)
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -24,6 +24,8 @@ for step in "$@"; do
     bench)   run bench 400 python bench.py ;;
     bench12) run bench12 400 python bench.py --eps 1e-12 --batch 4096 --steps 4 --warmup 1 --no-cpu-baseline ;;
     lone)    run lone 120 python tools/try_single.py ;;
+    lonecoop) AQ_COOP=1 run lone_coop 120 python tools/try_single.py ;;
+    shared2) BENCH_SHARED_GPU=1 run shared2 400 python bench.py --gpus 2 --steps 4 --warmup 1 --c3-n 131072 ;;
     diag)    run diag_1e10 120 python tools/diag_single.py --eps 1e-10 && run diag_1task 120 python tools/diag_single.py --eps 1e30 ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     xcd)     run xcd_start 120 python tools/xcd_start.py ;;

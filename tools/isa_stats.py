@@ -6,6 +6,7 @@ the v_rcp_f64 of the division), and prints its instruction classes: FP64 VALU, o
 LDS, branches. VGPR / SGPR / LDS usage come from the resource-usage remarks.
 
   python tools/isa_stats.py [--kernel _ZN2aq8k_streamILi0ELb0ELb0ELb0EEEvNS_12StreamParamsE] [-D...]
+  python tools/isa_stats.py --sizes [-D...]     # code bytes of every k_stream instance (device object)
 """
 import argparse
 import os
@@ -26,6 +27,28 @@ def compile_asm(defs, out):
     if r.returncode:
         sys.exit(r.stderr[-3000:])
     return r.stderr
+
+
+def code_sizes(defs):
+    """Machine-code bytes of every k_stream instance: a device-only object, its symbol sizes."""
+    d = tempfile.mkdtemp()
+    obj = os.path.join(d, "k.o")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-c",
+           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "--cuda-device-only", "--no-gpu-bundle-output", "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(ROOT, "ppls_amd", "csrc"),
+           '-DAQ_USER_F_HEADER="%s"' % os.path.join(ROOT, "ppls_amd", "csrc", "plugins", "aq_user_gauss.h"),
+           "-o", obj] + defs + [os.path.join(ROOT, "ppls_amd", "csrc", "aquad.hip")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode:
+        sys.exit(r.stderr[-3000:])
+    sym = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-sW", "--demangle", obj], capture_output=True,
+                         text=True, check=True).stdout
+    out = {}
+    for ln in sym.splitlines():
+        f = ln.split(None, 7)   # Num: Value Size Type Bind Vis Ndx Name
+        if len(f) == 8 and f[3] == "FUNC" and "k_stream" in f[7] and not f[7].endswith("(.kd)"):
+            out[f[7]] = int(f[2])
+    return out
 
 
 def classify(ins):
@@ -56,7 +79,13 @@ def main():
     ap.add_argument("--first-backedge", action="store_true",
                     help="bottom-tested loop: count up to the first conditional back-edge")
     ap.add_argument("--keep", help="also write the kernel's assembly (with labels) to this file")
+    ap.add_argument("--sizes", action="store_true", help="print the code bytes of every k_stream instance")
     a = ap.parse_args()
+    if a.sizes:
+        sz = code_sizes(["-D" + x for x in a.D])
+        for k in sorted(sz):
+            print("%7d B  %s" % (sz[k], k))
+        return
     d = tempfile.mkdtemp()
     out = os.path.join(d, "k.s")
     remarks = compile_asm(["-D" + x for x in a.D] + [y for m in a.mllvm for y in ("-mllvm", m)], out)
