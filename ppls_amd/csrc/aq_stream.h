@@ -7,11 +7,12 @@
 //     (:187), so it is not stored; dt = depth | SPAN_BIT | integral << 16. A pair is six 8-byte LDS
 //     fields for two tasks, and it hands every lane two independent evaluations: the K=2 cosh chains
 //     interleave (aq_libm.h cosh_main_k).
-//   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of pairs. A round pops
-//     <= 64 pairs, evaluates F at both midpoints in FP64 (glibc-exact cosh), applies the reference's
-//     refine test (:191) to both tasks and pushes each refining task's children as a new pair, with a
-//     ballot / mbcnt compaction: no workgroup barrier, no HBM traffic. Rounds run in bursts with
-//     all ring state wave-uniform (SGPRs).
+//   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of pairs, and each of its
+//     lanes carries one pair in registers. A round fills the idle lanes from the ring, evaluates F at
+//     both midpoints of every held pair in FP64 (glibc-exact cosh), applies the reference's refine
+//     test (:191) to both tasks, keeps task 0's children as the lane's next pair and pushes task 1's
+//     onto the ring, with a ballot / mbcnt compaction: no workgroup barrier, no HBM traffic. Rounds
+//     run in bursts with all ring state wave-uniform (SGPRs).
 //   * ring overflow goes to the wave's private HBM cellar (no lock; prefetched back when the ring
 //     runs low); a locked LDS pool feeds idle sibling waves; an HBM ticket queue of pair chunks moves
 //     work across CUs (what the bag of tasks is for), driven by one elected leader wave per idle
@@ -492,50 +493,49 @@ __device__ __forceinline__ double2 sload_bounds(const double2* base, int p) {
     return make_double2(__hiloint2double((int)r.y, (int)r.x), __hiloint2double((int)r.w, (int)r.z));
 }
 
-// One slot's six fields from / to ONE LDS address (the slot's a, in bytes): three ds_read2st64_b64
-// / ds_write2st64_b64 at 0 / 50 / 100 / 150 / 200 / 250 x 512 B (LREC = 3200 slots of 8 B per
-// field). The pop waits for its own reads (lgkmcnt(0)) inside the asm -- the compiler cannot count
-// LDS operations it does not see -- and the "memory" clobbers keep the compiler's own LDS accesses
-// on their side of both.
-static_assert(LREC * 8 == 50 * 512, "lds_pop6w / lds_push6x2 assume 50 x 512 B per field");
-// The pair word comes back as the raw 8-byte field (dt in its low half).
-__device__ __forceinline__ void lds_pop6w(unsigned addr, double& a, double& b, double& fa, double& fm, double& fb,
-                                          unsigned long long& dtw) {
-    f64x2 ab, ff, fd;
+// One slot's six fields from / to ONE LDS address (the slot's a, in bytes): the fields lie at 0 / 50 /
+// 100 / 150 / 200 / 250 x 512 B (LREC = 3200 slots of 8 B per field), the offsets of three
+// ds_write2st64_b64 / ds_read2st64_b64 (and of six ds_read_b64 from two bases). The pops wait for
+// their own reads (lgkmcnt(0)) inside the asm -- the compiler cannot count LDS operations it does not
+// see -- and the "memory" clobbers keep the compiler's own LDS accesses on their side of both.
+static_assert(LREC * 8 == 50 * 512, "the pair moves assume 50 x 512 B per field");
+// The carried round's LDS moves: a pop into the lanes of mask m only (the other lanes keep
+// their registers: "+v"), and a push of one pair from the lanes of m -- exec set around the three
+// accesses, no branch.
+// The pop reads the six fields as six ds_read_b64 (2 LDS-array cycles each, 256 B/clk; a
+// ds_read2st64_b64 takes 8 for two fields, 128 B/clk -- MI355X_MICROARCH.md §LDS) into six
+// independent registers (no 4-register tuple for the allocator to assemble each round); the 16-bit
+// offset reaches fields 0-2 from addr and 3-5 from addr2 = addr + 150 x 512 B.
+__device__ __forceinline__ void lds_pop6_masked(unsigned long long m, unsigned addr, unsigned addr2, double& a,
+                                                double& b, double& fa, double& fm, double& fb, double& dw) {
+    unsigned long long saved;
     asm volatile(
-        "ds_read2st64_b64 %0, %3 offset1:50\n\t"
-        "ds_read2st64_b64 %1, %3 offset0:100 offset1:150\n\t"
-        "ds_read2st64_b64 %2, %3 offset0:200 offset1:250\n\t"
+        "s_mov_b64 %6, exec\n\t"
+        "s_mov_b64 exec, %7\n\t"
+        "ds_read_b64 %0, %8\n\t"
+        "ds_read_b64 %1, %8 offset:25600\n\t"
+        "ds_read_b64 %2, %8 offset:51200\n\t"
+        "ds_read_b64 %3, %9\n\t"
+        "ds_read_b64 %4, %9 offset:25600\n\t"
+        "ds_read_b64 %5, %9 offset:51200\n\t"
+        "s_mov_b64 exec, %6\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(ab), "=&v"(ff), "=&v"(fd)
-        : "v"(addr)
+        : "+v"(a), "+v"(b), "+v"(fa), "+v"(fm), "+v"(fb), "+v"(dw), "=&s"(saved)
+        : "s"(m), "v"(addr), "v"(addr2)
         : "memory");
-    a = ab.x; b = ab.y; fa = ff.x; fm = ff.y; fb = fd.x;
-    dtw = (unsigned long long)__double_as_longlong(fd.y);
 }
-// A round's two pushes (the children pairs of the refining tasks 0 / 1) under the exec masks m0 / m1,
-// with no branch: exec is saved once, set to each mask around its three writes and restored (an empty
-// mask makes the writes no-ops). The compiler's form -- s_and_saveexec, s_cbranch_execz, s_or_b64
-// exec per push -- put two branches in every round. Every mask is a subset of the caller's exec.
-__device__ __forceinline__ void lds_push6x2(unsigned long long m0, unsigned a0, double x0, double y0, double u0,
-                                            double v0, double w0, unsigned long long m1, unsigned a1, double x1,
-                                            double y1, double u1, double v1, double w1, unsigned dt) {
-    const double dw = __longlong_as_double((long long)dt);
+__device__ __forceinline__ void lds_push6_masked(unsigned long long m, unsigned addr, double x0, double x1, double x2,
+                                                 double x3, double x4, double x5) {
     unsigned long long saved;
     asm volatile(
         "s_mov_b64 %0, exec\n\t"
         "s_mov_b64 exec, %1\n\t"
-        "ds_write2st64_b64 %3, %5, %6 offset1:50\n\t"
-        "ds_write2st64_b64 %3, %7, %8 offset0:100 offset1:150\n\t"
-        "ds_write2st64_b64 %3, %9, %15 offset0:200 offset1:250\n\t"
-        "s_mov_b64 exec, %2\n\t"
-        "ds_write2st64_b64 %4, %10, %11 offset1:50\n\t"
-        "ds_write2st64_b64 %4, %12, %13 offset0:100 offset1:150\n\t"
-        "ds_write2st64_b64 %4, %14, %15 offset0:200 offset1:250\n\t"
+        "ds_write2st64_b64 %2, %3, %4 offset1:50\n\t"
+        "ds_write2st64_b64 %2, %5, %6 offset0:100 offset1:150\n\t"
+        "ds_write2st64_b64 %2, %7, %8 offset0:200 offset1:250\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(saved)
-        : "s"(m0), "s"(m1), "v"(a0), "v"(a1), "v"(x0), "v"(y0), "v"(u0), "v"(v0), "v"(w0), "v"(x1), "v"(y1),
-          "v"(u1), "v"(v1), "v"(w1), "v"(dw)
+        : "s"(m), "v"(addr), "v"(x0), "v"(x1), "v"(x2), "v"(x3), "v"(x4), "v"(x5)
         : "memory");
 }
 // One slot's six fields in registers (cellar moves): lds_issue6 only ISSUES the three
@@ -1368,22 +1368,33 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             __builtin_amdgcn_wave_barrier();
         }
 
-        // ---- a burst of rounds: the hot loop. It runs while the ring neither empties nor nears
-        //      overflow, no cellar prefetch is in flight or due, and the next round is not a
-        //      give / poll check round: everything it touches besides the pairs is wave-uniform.
+        // ---- a burst of rounds: the hot loop. It runs while the wave's pairs (ring + held) neither
+        //      run out nor near overflow, no cellar move is due, and the next round is not a give /
+        //      poll check round: everything it touches besides the pairs is wave-uniform.
         // the burst's state, re-asserted uniform (readfirstlane) once per burst: the outer loop's many
         // paths leave the compiler unsure, and a "divergent" ring index turns every round's index
         // arithmetic and the loop exit into VALU / exec-mask work
         unsigned b_top = uni(top), b_size = uni(size), b_poll = uni(poll_ctr);
-        const unsigned b_top0 = b_top;
-        unsigned b_n = 0;                 // pairs popped in this burst (2 tasks each)
+        unsigned b_n = 0;                 // pairs evaluated in this burst (2 tasks each)
         unsigned long long b_dv = 0;      // lanes that met the depth cap with a refining task
         unsigned b_bot = uni(bot), b_ctop = uni(ctop), b_pf = uni(pf_n);
         bool b_mixed = uni(mixed);
-        // the burst goes on while lo < size <= hi and the next round is no give / poll round:
-        // lo = PF_BELOW while a prefetch is in flight (land it), PF_ISSUE while the cellar holds pairs
-        // and none is (issue one), else 0 (stop when empty); hi = WCAP - 64 (near overflow). One
-        // subtract and one compare per round, and one compare for the round counter.
+        // Carried pairs (r04). Every lane keeps ONE pair in registers from round to round (b_am: the
+        // lanes that hold one). A round first fills the idle lanes from the ring's top (one masked
+        // pop), evaluates both tasks of every held pair, pushes ONE child pair per lane -- task 1's,
+        // when it refines -- and keeps task 0's children as the lane's next pair (a depth-first walk
+        // per lane, the ring holding the right siblings). Three pair writes per round where the
+        // popped-pairs round made six: the writes' VGPR-to-LDS transfer and LDS-array cycles are the
+        // CU's second bottleneck beside the VALU (83 LDS-array cycles per wave-round, active 59 % of
+        // the kernel's cycles: profiles/r04_pmc_lds; r04 A/B -6.5 %, profiles/r04_ab). The pop is six
+        // ds_read_b64 (12 array cycles) rather than three ds_read2st64_b64 (24). The window, the cellar lines and the accounting
+        // count S = ring + held pairs; a burst starts with every pair in the ring and ends by pushing
+        // the held ones back on top. Capacity: a round moves at most one pair per active lane into the
+        // ring, so the ring never holds more than S at a round's start; S <= WCAP - 64 then leaves
+        // room for the round (S grows by <= 64) and the final push.
+        unsigned b_S = b_size, b_S0 = b_size;   // ring + held; the accounting base (moves with the cellar)
+        unsigned long long b_am = 0;
+        double ca = 0.0, cb = 0.0, cfa = 0.0, cfm = 0.0, cfb = 0.0, cdw = 0.0;   // the held pair (cdw: the dt word)
         unsigned b_lo1, b_span;
         auto window = [&]() {
             b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : (b_ctop > 0u ? (unsigned)PF_ISSUE : 0u)) + 1u;
@@ -1391,65 +1402,50 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         };
         window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
-        unsigned b_rem = b_max;   // rounds left up to the give / poll round (counted down: no copy of a
-                                  // round counter per round)
+        unsigned b_rem = b_max;
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // (see below: no wait in front of every round's pop)
         bool b_go;
-        for (;;) {   // the burst: runs of rounds (the inner loop, its exit one compare), and the cellar
-                     // moves at the window's edges between them
         for (;;) {
-            // ---- one round: pop up to 64 pairs from the top of this wave's ring, one per lane; both
-            //      tasks of a pair are evaluated together (two interleaved cosh chains)
+        for (;;) {
             unsigned long long c0 = 0, c1 = 0;
             if constexpr (DIAG) c0 = clk();
-            const unsigned n = min(b_size, 64u);
-            const unsigned b0 = b_top - n;
-            const unsigned b0s = ring_slot(b0);                 // uniform (scalar) modulo
-            // every lane reads a slot (lanes >= n a stale, harmless one): no per-lane defaults
-            double pa, pb, pfa, pfm, pfb;
-            unsigned long long dtw;   // the pair word's 8-byte field (dt in its low half)
-            asm volatile("s_setprio 3");   // the pop and the F chains ahead of the siblings' tails
-            lds_pop6w(ring_addr(ring8, b0s + lane, ring_vmask), pa, pb, pfa, pfm, pfb, dtw);
+            asm volatile("s_setprio 3");
+            // ---- fill: the idle lanes take the ring's top k pairs (rank j among the idle lanes)
+            const unsigned long long need = ~b_am;
+            const unsigned k = min((unsigned)__popcll(need), b_top - b_bot);
+            const unsigned jr = mbcnt(need);
+            const unsigned long long fmsk = __ballot(jr < k) & need;
+            b_top -= k;
+            const unsigned paddr = ring_addr(ring8, ring_slot(b_top) + jr, ring_vmask);
+            lds_pop6_masked(fmsk, paddr, paddr + 3u * 50u * 512u, ca, cb, cfa, cfm, cfb, cdw);
+            const unsigned long long am = b_am | fmsk;
+            const unsigned na = (unsigned)__popcll(am);
+            const double pa = ca, pb = cb, pfa = cfa, pfm = cfm, pfb = cfb;
+            const unsigned long long dtw = (unsigned long long)__double_as_longlong(cdw);
             const unsigned dt = (unsigned)dtw;
             Step2 st[2];
-            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
-            // byte test for the pair): an SDWA compare on dt's second byte -- written out, since the
-            // compiler turns the byte test into an and plus a compare
             unsigned long long nospan = 0ull;
             if constexpr (FID == F_COSH4)
                 asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
-            // (a scalar mask of lanes 0..n-1 in place of this ballot: one v_cmp fewer, five SALU more,
-            // measured 0.9 % slower)
-            const unsigned long long am = __ballot(lane < n);
-            // pa, pb: the pair's HALVED endpoints (pair_step_halves); pm = the parent's midpoint (:187)
             double pm, hm;
             pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
             asm volatile("s_setprio 0");
-            // refine (:191) unless the depth cap is reached (then the task is dropped, error reported).
-            // Wave masks are ballots of plain comparisons combined with scalar ops: a ballot of a
-            // compound predicate would be materialised per lane (v_cndmask + v_cmp) first.
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
             unsigned long long okm = am;
             if constexpr (!burst_cap) {
                 const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
                 okm = am & dm;
-                // tasks at the depth cap that would refine (checked at burst end; a cap lane is rare)
                 const unsigned long long atcap = am & ~dm;
                 if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
             }
-            // accounting (:199 -> :149, :162). A ring only ever holds pairs of one integral, the wave's
-            // current `tag` (seeds, pool takes and chunks switch it, with a flush, before they land):
-            // counts are wave-level, the area one masked add per accepted task.
             const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
-            b_n += n;   // tasks 2n; accepted: counted once per burst from the ring's growth (below)
-            // a lane's own few leaves (rounding far below the total's ulp), added under the leaf masks
-            // (doubled areas: halved at flush); the deepest pair popped, under the active mask -- or,
-            // with the per-burst depth cap, the deepest refining pair
+            b_n += na;   // tasks 2 na; accepted: once per burst from the growth of S (below)
             const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-            const unsigned cdt = dt + 1u;   // depth + 1, same integral
+            const unsigned long long cdtw = dtw + 1ull;   // depth + 1, same integral
+            const unsigned cdt = (unsigned)cdtw;
             masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
                         burst_cap ? (mask0 | mask1) : am);
-            if constexpr (DIAG) {   // the one-integral-per-ring invariant holds by construction (pool
-                                    // takes and seeds switch the tag); checked in diagnostic builds
+            if constexpr (DIAG) {
                 const int rtag = (int)(dt >> TAG_SHIFT);
                 b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
             }
@@ -1462,57 +1458,55 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
             }
             if constexpr (DIAG) c1 = clk();
-            // each refining task pushes its children as one pair (:192-197), compacted by mbcnt
-            // seeded with the round's base slot (the counts start at b0s / b0s + cnt0); both pushes
-            // under exec masks, no branch (lds_push6x2)
-            const unsigned cnt0 = (unsigned)__popcll(mask0);
-            lds_push6x2(mask0, ring_addr(ring8, b0s + mbcnt(mask0), ring_vmask), pa, hm, pfa, st[0].fmid, pfm,
-                        mask1, ring_addr(ring8, b0s + cnt0 + mbcnt(mask1), ring_vmask), hm, pb, pfm, st[1].fmid, pfb,
-                        cdt);
-            b_top = b0 + cnt0 + (unsigned)__popcll(mask1);
+            // ---- task 1's children [m, b] go on the ring (:192-197); task 0's [a, m] stay in the lane
+            lds_push6_masked(mask1, ring_addr(ring8, ring_slot(b_top) + mbcnt(mask1), ring_vmask), hm, pb, pfm,
+                             st[1].fmid, pfb, __longlong_as_double((long long)cdtw));
+            b_top += (unsigned)__popcll(mask1);
+            cb = hm;
+            cfb = pfm;
+            cfm = st[0].fmid;
+            cdw = __longlong_as_double((long long)cdtw);
+            b_am = mask0;
             if constexpr (DIAG) {
                 if (lane == 0) {
                     const unsigned long long c2 = clk();
                     atomicAdd(&s_dg[DG_ROUNDS], 1ull);
-                    atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)n);
+                    atomicAdd(&s_dg[DG_ACTIVE_LANES], (unsigned long long)na);
                     atomicAdd(&s_dg[DG_C_ROUND], c2 - c0);
                     atomicAdd(&s_dg[DG_C_EVAL], c1 - c0);
-                    atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_size);
+                    atomicMax(&s_dg[DG_MAX_RING], (unsigned long long)b_S);
                     atomicMax(&s_dg[DG_T_LAST_ROUND], rtc());
+                    atomicAdd(&s_dg[DG_ACTIVE_TASKS], 2ull * na);
                 }
-                const unsigned nt = 2u * n;
-                if (lane == 0) atomicAdd(&s_dg[DG_ACTIVE_TASKS], (unsigned long long)nt);
             }
-            b_size = b_top - b_bot;
+            b_S = (b_top - b_bot) + (unsigned)__popcll(mask0);
             --b_rem;
-            // one compare: the give / poll round closes the size window (opaque, so the compiler does
-            // not split it back into two conditions joined by SALU selects)
             unsigned span_r = b_rem != 0u ? b_span : 0u;
             asm("" : "+s"(span_r));
-            b_go = b_size - b_lo1 < span_r;
+            b_go = b_S - b_lo1 < span_r;
             __builtin_amdgcn_wave_barrier();
             if (!b_go) break;
         }
-            // the edge test reads b_rem through an opaque copy: otherwise the compiler keeps `b_rem != 0`
-            // as a materialised lane mask across the round's select
             unsigned b_re = b_rem;
             asm volatile("" : "+s"(b_re));
-            const unsigned sz = b_size;
+            const unsigned sz = b_S;
             if (b_re != 0u && sz != 0u) {
-                // a cellar edge (not the give / poll round, not an empty ring): move the chunk here
-                // and go on (the cellar-full spill and the pool / queue fallbacks stay outside)
+                // a cellar edge: S > WCAP - 64 leaves >= WCAP - 128 >= SPILL pairs in the ring; S <=
+                // PF_BELOW leaves the ring room for the landing
                 if (sz > (unsigned)(WCAP - 64)) {
                     if (b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
-                        if (b_pf) {   // cancel the prefetch in flight (its pairs never left the cellar)
+                        if (b_pf) {
                             b_ctop += b_pf;
                             b_pf = 0;
                         }
                         spill_to_cellar(b_bot, b_ctop);
                         b_ctop += (unsigned)SPILL;
                         b_bot += (unsigned)SPILL;
+                        b_S -= (unsigned)SPILL;
+                        b_S0 -= (unsigned)SPILL;
                         b_go = true;
                     }
-                } else if (b_pf) {                   // down to PF_BELOW: land the prefetch
+                } else if (b_pf) {
                     if (b_bot < 64u) {
                         b_bot += (unsigned)WCAP;
                         b_top += (unsigned)WCAP;
@@ -1520,33 +1514,36 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     b_bot -= b_pf;
                     if (lane < b_pf) lds_store6(ring_addr(ring8, ring_slot(b_bot) + lane, ring_vmask), pf);
                     if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_PREFETCH], (unsigned long long)b_pf); }
+                    b_S += b_pf;
+                    b_S0 += b_pf;
                     b_pf = 0;
                     b_go = true;
-                } else if (b_ctop > 0u) {   // down to PF_ISSUE: issue a prefetch
+                } else if (b_ctop > 0u) {
                     b_pf = 64u;
                     b_ctop -= 64u;
                     pf = chunk_load(&cel->c[b_ctop / 64u], lane);
                     b_go = true;
                 }
-                if (b_go) {
-                    window();
-                    b_size = b_top - b_bot;
-                }
+                if (b_go) window();
             }
             __builtin_amdgcn_wave_barrier();
             if (!b_go) break;
         }
+        // the held pairs back on top of the ring
+        lds_push6_masked(b_am, ring_addr(ring8, ring_slot(b_top) + mbcnt(b_am), ring_vmask), ca, cb, cfa, cfm, cfb,
+                         cdw);
+        b_top += (unsigned)__popcll(b_am);
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;
         b_poll += (b_max - b_rem) - 1u;   // every round but the burst's last advances the give / poll counter
         top = b_top;
         poll_ctr = b_poll;
-        // every refining task pushed one pair, so pushes = (b_top - b_top0) + b_n and the accepted
-        // tasks are 2 b_n - pushes = b_n - (b_top - b_top0) (a burst that met the depth cap dropped
-        // tasks as well: those count as accepted here, and the launch reports ERRB_DEPTH)
+        // a round with na held pairs evaluates 2 na tasks; each refining task adds one pair to S and
+        // each evaluated pair leaves it, so accepted = 2 na - refining = na - (growth of S); summed over
+        // the burst: b_n - (S_end - S_start), the cellar moves taken out of S_start as they happen
         acc.ut += 2u * b_n;
-        acc.ul += b_n - (b_top - b_top0);
+        acc.ul += b_n - ((b_top - b_bot) - b_S0);
         dd_add(acc.hi, acc.lo, acc.r);   // the burst's lane partial, exactly into the double-double
         acc.r = 0.0;
         if (b_dv) err |= ERRB_DEPTH;

@@ -123,7 +123,7 @@ def main():
     best = None
     for key in keys:
         lines = [x for b in blocks if inloop(b, key) for x in b[3]]
-        if any("v_rcp_f64" in x for x in lines) and any("v_mbcnt_lo" in x for x in lines) and any("ds_read2st64" in x for x in lines):
+        if any("v_rcp_f64" in x for x in lines) and any("v_mbcnt_lo" in x for x in lines) and any("st64" in x for x in lines):
             if best is None or key[1] > best[1]:
                 best = key
     if best is None:
