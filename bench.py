@@ -5,10 +5,13 @@ Workload (BASELINE.json configs[1]): F(x)=cosh(x)^4 (aquadPartA.c:46) over [0,5]
 EPSILON=1e-10 -- 1 464 273 tasks, 732 137 accepted subintervals per integral. One step = one batch
 of B (default 32768) such integrals through the hot path (persistent on-device farmer,
 ppls_amd/csrc/aq_stream.h). With N ranks (one process per GPU, torch.distributed backend "nccl" =
-RCCL) every integral is sharded: rank r evaluates shard r of N of each integral (the domain split
-into subranges per GPU; strong scaling, total work fixed), and a rank packs up to N batches into
-one persistent launch (up to the 65536 integrals a launch holds). The partial results of the K
-timed steps are combined with ONE all-reduce inside the timed region. Launches are pipelined
+RCCL) every integral is sharded: each rank evaluates one shard of N of each integral (the domain
+split into subranges per GPU; strong scaling, total work fixed) -- rank r shard (r + i) mod N of the
+launch's i-th integral, so every rank gets every shard equally often and the snake partition's
+per-shard skew (1.5 % at 8 shards) cancels -- and a rank packs N batches into one persistent launch
+(a launch holds up to 262144 integrals: N x 32768 shards of 1/N each, the work of one GPU's
+32768-integral launch, whatever N <= 8). The partial results of the K timed steps are combined with
+ONE all-reduce inside the timed region. Launches are pipelined
 (no host sync between them); every integral's counts are verified bit-exactly and its area to
 1e-12 relative against the golden tree after timing.
 
@@ -366,9 +369,13 @@ def main(argv=None):
     lb = max(1, min(world, cap // B))
 
     def launch(m, eps=args.eps):
-        # m integrals of the workload in one persistent launch (slots 0..m-1), this rank's shard
-        in_turn(lambda: ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), eps, first_slot=0, shard=rank,
-                                                 nshards=world))
+        # m integrals of the workload in one persistent launch (slots 0..m-1), this rank's shards: the
+        # i-th integral's shard (rank + i) mod N (every rank holds each shard of 1/N of the integrals)
+        if world == 1:
+            in_turn(lambda: ctx.integrate_many_async(np.zeros(m), np.full(m, 5.0), eps, first_slot=0))
+        else:
+            sh = (rank + np.arange(m)) % world
+            in_turn(lambda: ctx.integrate_mixed_async(np.zeros(m), np.full(m, 5.0), sh, world, eps, first_slot=0))
 
     # single-integral latency (one integral per launch), reported beside the throughput: on one GPU
     # the kernel of the synchronous call a user makes for one integral (aq_integrate: its result slot
@@ -449,9 +456,8 @@ def main(argv=None):
     tasks_total = float(tot[:, 1].sum())
     f_evals = tasks_total + 2 * n_int   # algorithmic F evaluations: 1 per task + F(A), F(B) per integral
 
-    # this rank's share of the tasks per launch, for the roofline of its kernel
-    mine = ctx.fetch(0)
-    tasks_per_launch = mine.tasks * per_launch
+    # this rank's tasks per launch (its shards), for the roofline of its kernel
+    tasks_per_launch = float(my_tasks.item()) / max(launches, 1)
     achieved = FLOP_PER_TASK * tasks_per_launch / (kern_avg_ms * 1e-3) if kern_avg_ms > 0 else 0.0
 
     secondary = None
@@ -476,7 +482,7 @@ def main(argv=None):
 
 def c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist):
     """BASELINE configs[2]: 1 M splitmix64-bounded integrals at EPSILON=1e-10, contiguous whole-integral
-    blocks per rank through aq_integrate_batch (65536 integrals per persistent launch)."""
+    blocks per rank through aq_integrate_batch (up to 262144 integrals per persistent launch)."""
     import numpy as np
     import torch
     eps = 1e-10

@@ -126,13 +126,21 @@ constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from
 constexpr int PCU_MAXK = 12;
 constexpr int PCU_ROW = PCU_MAXK - 1;   // per-CU LDS rows: tags < k < PCU_MAXK
 constexpr int STATIC_MAXK = 16;     // launches of fewer integrals (unsharded): one share per wave, static stride
-constexpr int MAXK = 65536;         // max integrals per launch (tag: the pair word's high 16 bits)
-// The pair word dt: bits 0-7 the pair's depth (the depth of its two tasks), bit 8 SPAN_BIT, bits
-// 16-31 the integral (tag). SPAN_BIT (cosh4): the pair's interval lies where glibc's cosh takes its
-// exp path (cosh_main_span) -- set at seeding, inherited by the children (sub-intervals), so a
-// round tests one byte instead of two words.
-constexpr unsigned SPAN_BIT = 1u << 8;
-constexpr int TAG_SHIFT = 16;
+// The pair word dt: bits 0-7 the pair's depth (the depth of its two tasks), bits 8-30 the integral
+// (tag), bit 31 SPAN_BIT. SPAN_BIT (cosh4): the pair's interval lies where glibc's cosh takes its exp
+// path (cosh_main_span) -- set at seeding, inherited by the children (sub-intervals), so a round tests
+// the word's sign instead of two words.
+constexpr unsigned SPAN_BIT = 1u << 31;
+constexpr int TAG_SHIFT = 8;
+constexpr unsigned TAG_MASK = (1u << 23) - 1u;
+__host__ __device__ constexpr unsigned dt_tag(unsigned dt) { return (dt >> TAG_SHIFT) & TAG_MASK; }
+// max integrals per launch: 8 x 32768, so that N = 8 ranks holding 1/8 of each integral of a batch
+// pack the same work into one launch as one GPU does with the whole batch (r04)
+constexpr int MAXK = 1 << 18;
+static_assert((unsigned)MAXK - 1u <= TAG_MASK, "the tag field must hold every integral of a launch");
+// slots whose per-CU launches keep per-workgroup words (parts), plus one row for the sync slot
+constexpr int NPARTS = 65536;
+__host__ __device__ __forceinline__ size_t parts_row(int slot) { return slot < NPARTS ? (size_t)slot : (size_t)NPARTS; }
 #ifndef AQ_GSPLIT_DEFAULT
 #define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
@@ -181,13 +189,13 @@ static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed pref
 // lane, the deepest REFINING pair it saw (masked max, as before over the popped pairs); the burst's
 // end tests that against max_depth - 1 -- one compare per burst instead of a compare, two SALU and a
 // branch per round. A burst runs at most give_rounds rounds, so pairs past the cap are at most
-// give_rounds levels deeper: the depth byte (dt's low 8 bits) cannot carry into SPAN_BIT while
+// give_rounds levels deeper: the depth byte (dt's low 8 bits) cannot carry into the tag while
 // (AQ_MAX_LEVELS - 1) + give_rounds < 256 (asserted below). A wave that finds the cap exceeded drops
 // its ring and cellar before anything else can see them: nothing deeper than the cap ever reaches the
 // pool or the HBM queue. The run is then invalid (ERRB_DEPTH), as before. (The histogram instance
 // keeps the per-round test.)
 static_assert((AQ_MAX_LEVELS - 1) + (GIVE_ROUNDS > SKEWED_GIVE ? GIVE_ROUNDS : SKEWED_GIVE) < 256,
-              "a burst's pairs past the depth cap must not carry the depth byte into SPAN_BIT");
+              "a burst's pairs past the depth cap must not carry the depth byte into the tag");
 constexpr int SPILL = 64;   // pairs a ring above WCAP - 64 moves to its cellar at once (r02 A/B: 128 at once
                             // 4.0 % slower at eps 1e-10, 6.5 % at 1e-12: more refills)
 
@@ -327,7 +335,8 @@ struct StreamParams {
     Ctl* ctls;                      // per-slot control blocks
     QCtl* q;                        // this launch's queue and termination count (all-zero at launch)
     QCtl* q_next;                   // the next launch's: workgroup 0 zeroes it
-    unsigned long long* parts;      // [2 * (slot * gridDim.x + wg) + 0/1]: per-CU launches' counts (slot_counts)
+    unsigned long long* parts;      // per-CU launches' counts (slot_counts): integral p's row at
+                                    // [2 * (p * gridDim.x + wg) + 0/1] (the first slot's parts row)
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
     unsigned long long* cu_acc;     // [AQ_CU_SLOTS] tasks per hardware CU slot, summed over launches
                                     // (every launch: the farmer's tasks_per_process, :162, per CU)
@@ -836,11 +845,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         const unsigned pb = S.pbot;
                         // a ring holds pairs of ONE integral (the rounds count without per-lane tags):
                         // take the leading run of pool pairs that share the first pair's integral
-                        ptag = (int)uni(s_dt[POOL0 + (pb & (PCAP - 1))] >> TAG_SHIFT);
+                        ptag = (int)uni(dt_tag(s_dt[POOL0 + (pb & (PCAP - 1))]));
                         for (unsigned q0 = 0; q0 < k; q0 += 64) {
                             const unsigned q = q0 + lane;
                             const unsigned long long bad =
-                                __ballot(q < k && (int)(s_dt[POOL0 + ((pb + q) & (PCAP - 1))] >> TAG_SHIFT) != ptag);
+                                __ballot(q < k && (int)dt_tag(s_dt[POOL0 + ((pb + q) & (PCAP - 1))]) != ptag);
                             if (bad) {
                                 k = q0 + (unsigned)__builtin_ctzll(bad);
                                 break;
@@ -1424,9 +1433,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             const unsigned long long dtw = (unsigned long long)__double_as_longlong(cdw);
             const unsigned dt = (unsigned)dtw;
             Step2 st[2];
+            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
+            // sign test of the pair word)
             unsigned long long nospan = 0ull;
-            if constexpr (FID == F_COSH4)
-                asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:BYTE_1 src1_sel:DWORD" : "=s"(nospan) : "v"(dt), "v"(0u) : "vcc");
+            if constexpr (FID == F_COSH4) nospan = __ballot((int)dt >= 0);
             double pm, hm;
             pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
             asm volatile("s_setprio 0");
@@ -1446,7 +1456,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
                         burst_cap ? (mask0 | mask1) : am);
             if constexpr (DIAG) {
-                const int rtag = (int)(dt >> TAG_SHIFT);
+                const int rtag = (int)dt_tag(dt);
                 b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
             }
             if (HIST) {
@@ -1602,7 +1612,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned long long t = __hip_atomic_load(&s_pc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned long long l = __hip_atomic_load(&s_pc[PCU_ROW + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const unsigned m = (unsigned)__hip_atomic_load(&s_pc[2 * PCU_ROW + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                unsigned long long* wp = P.parts + 2 * ((size_t)(P.first_slot + p) * gridDim.x + bid);
+                unsigned long long* wp = P.parts + 2 * ((size_t)p * gridDim.x + bid);
                 wp[0] = pack_cu(t, cu);
                 wp[1] = (l << 8) | (unsigned long long)(m & 255u);
                 if (bid == 0) P.ctls[P.first_slot + p].sums.pcu = 1u;

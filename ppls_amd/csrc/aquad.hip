@@ -489,7 +489,7 @@ __global__ __launch_bounds__(64) void k_gather(const Ctl* __restrict__ ctls, con
     if (i >= n) return;
     const int slot = (first + i) % nslots;
     const Ctl& c = ctls[slot];
-    const Counts k = slot_counts(c.sums, parts + 2 * (size_t)slot * grid, grid);
+    const Counts k = slot_counts(c.sums, parts + 2 * parts_row(slot) * grid, grid);
     double* o = out + 4 * (size_t)i;
     o[0] = xs_round(c.area);
     o[1] = (double)k.tasks;
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(64) void k_gather_exact(const Ctl* __restrict__ ctl
     long long* o = out + (size_t)AQ_EXACT_ROW * i;
     for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) o[k] = c.area.limb[k];
     if (threadIdx.x == 0) {
-        const Counts k = slot_counts(c.sums, parts + 2 * (size_t)slot * grid, grid);
+        const Counts k = slot_counts(c.sums, parts + 2 * parts_row(slot) * grid, grid);
         o[XS_LIMBS] = (long long)k.tasks;
         o[XS_LIMBS + 1] = (long long)k.leaves;
         o[XS_LIMBS + 2] = (long long)c.sums.spilled;
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(256) void k_pack_group(const Ctl* __restrict__ ctls
                                                     int slot, int grid, int with_parts, long long* __restrict__ sum_row,
                                                     unsigned long long* __restrict__ info) {
     const Ctl& c = ctls[slot];
-    const unsigned long long* wp = parts + 2 * (size_t)slot * grid;
+    const unsigned long long* wp = parts + 2 * parts_row(slot) * grid;
     for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) sum_row[k] = c.area.limb[k];
     for (int k = threadIdx.x; k < grid; k += blockDim.x) info[3 + k] = with_parts ? wp[2 * k] : 0ull;
     if (threadIdx.x == 0) {

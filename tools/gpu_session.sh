@@ -40,6 +40,7 @@ for step in "$@"; do
     lonevar) for so in ppls_amd/_build/${AB_GLOB_L:-libaquad_*.so}; do n=$(basename $so .so); AQ_LIB=$PWD/$so run lone_$n 120 python tools/try_single.py --reps 20; done ;;
     lonesplit) for g in 1 2 3 4; do AQ_GSPLIT=$g run lone_gsplit$g 120 python tools/try_single.py --reps 20; done ;;
     prof)    run prof 1000 bash tools/profile_round.sh "$TAG" ;;
+    pmclds)  run pmclds 300 bash tools/pmc_lds.sh "pmc_lds_$TAG" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -11,7 +11,7 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 ARGS=("$@")
-[ ${#ARGS[@]} -eq 0 ] && ARGS=(--no-cpu-baseline --no-single --steps 2 --warmup 1)
+[ ${#ARGS[@]} -eq 0 ] && ARGS=(--no-cpu-baseline --no-single --no-secondary --steps 8 --warmup 1)
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
     python3 "$ROOT/bench.py" "${ARGS[@]}" > "$OUT/bench_kt.json" 2> "$OUT/kt.err"
