@@ -39,8 +39,15 @@ namespace aq {
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
+// Pairs each lane carries (AQ_NP): 1 -- 12 waves per CU (3 per SIMD), 2 -- 8 waves per CU (2 per SIMD,
+// four interleaved F chains per lane, the VGPR budget of 2 waves)
+#ifndef AQ_NP
+#define AQ_NP 1
+#endif
+constexpr int NP = AQ_NP;
+static_assert(NP == 1 || NP == 2, "one or two carried pairs per lane");
 #ifndef AQ_PT
-#define AQ_PT 768
+#define AQ_PT (AQ_NP == 1 ? 768 : 512)
 #endif
 #ifndef AQ_WCAP
 #define AQ_WCAP 256
@@ -57,7 +64,9 @@ constexpr int WCAP = AQ_WCAP;       // per-wave LDS ring, pairs: a round pops <=
 // access; the pool went from 256 to 128 pairs to make room).
 constexpr int PCAP = 128;           // per-workgroup LDS pool ring, pairs (power of two)
 constexpr int DT_STRIDE = 2;        // dt words per slot (the low word of an 8-byte field)
-constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 3200 x 48 B = 150 KiB
+constexpr int LREC = 3200;          // LDS pair slots per field: 3200 x 48 B = 150 KiB (the pair moves' offsets
+                                    // assume it; with 8 waves the rings and pool use 2176 of them)
+static_assert(NW * WCAP + PCAP <= LREC, "the rings and the pool fit the pair block");
 constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = PCAP;            // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
 // the pair words of the LDS block: slot j's word at p[DT_STRIDE * j]
@@ -142,7 +151,9 @@ static_assert((unsigned)MAXK - 1u <= TAG_MASK, "the tag field must hold every in
 constexpr int NPARTS = 65536;
 __host__ __device__ __forceinline__ size_t parts_row(int slot) { return slot < NPARTS ? (size_t)slot : (size_t)NPARTS; }
 #ifndef AQ_GSPLIT_DEFAULT
-#define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
+// sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11,
+// 96 -> 1.803e11); a multiple of the waves per workgroup, so that it divides the launch's waves
+#define AQ_GSPLIT_DEFAULT (8 * (AQ_PT / 64))
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
 #ifndef AQ_LONE_GSPLIT
@@ -155,7 +166,10 @@ constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's 
 #endif
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
-constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
+// the burst window's top: a round moves at most NP pairs per lane into the ring (and the burst's end
+// the held ones), so S = ring + held <= WCAP - 64 NP at a round's start keeps the ring from overflowing
+constexpr int HI = WCAP - 64 * NP;
+constexpr int REFILL = HI;          // pairs a wave with an empty ring takes back from its cellar
 #ifndef AQ_PF_BELOW
 // r02 A/B (8192-integral launch, GIVE_ROUNDS 32): 112 28.39, 96 27.93, 80 27.57, 64 27.20, 48 28.18,
 // 32 30.25 ms, no prefetch 33.37 ms. The old 128 (= WCAP - 128) made a ring that had just spilled
@@ -171,10 +185,10 @@ constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetche
 // 80 % of the prefetches then have >= 2 rounds to arrive instead of 1). A ring that overflows while
 // they are in flight cancels them (the pairs are still in the cellar: only ctop moved) and spills.
 #ifndef AQ_PF_ISSUE
-#define AQ_PF_ISSUE 160   // r03 A/B (8192 x eps=1e-10): 96 -0.6 %, 128 -1.8 %, 160 -2.4 % vs landing after one round
+#define AQ_PF_ISSUE (AQ_NP == 1 ? 160 : 96)   // r03 A/B (8192 x eps=1e-10): 96 -0.6 %, 128 -1.8 %, 160 -2.4 % vs landing after one round
 #endif
 constexpr int PF_ISSUE = AQ_PF_ISSUE;
-static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
+static_assert(PF_ISSUE >= PF_BELOW && PF_ISSUE < HI && PF_BELOW + 64 <= HI, "a landed prefetch must leave the ring below the spill line");
 // In-burst cellar moves (r03): a round that leaves the burst's size window at a cellar edge -- above
 // the spill line, or down to the prefetch issue / landing line -- moves the chunk inside the burst
 // and the burst goes on, where round 2 left the burst for the outer loop (~60 VALU and ~70 SALU of
@@ -1252,7 +1266,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
         // ---- keep the ring from overflowing: its bottom 64 pairs go to the cellar, else the pool,
         //      else an HBM chunk
-        if (size > (unsigned)(WCAP - 64)) {
+        if (size > (unsigned)HI) {
             if (pf_n) {
                 // a prefetch in flight is cancelled: its pairs never left the cellar (the loads land in
                 // registers nobody reads; the next spill writes above them)
@@ -1399,15 +1413,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // ds_read_b64 (12 array cycles) rather than three ds_read2st64_b64 (24). The window, the cellar lines and the accounting
         // count S = ring + held pairs; a burst starts with every pair in the ring and ends by pushing
         // the held ones back on top. Capacity: a round moves at most one pair per active lane into the
-        // ring, so the ring never holds more than S at a round's start; S <= WCAP - 64 then leaves
-        // room for the round (S grows by <= 64) and the final push.
+        // ring, so the ring never holds more than S at a round's start; S <= HI = WCAP - 64 NP then
+        // leaves room for the round (S grows by <= 64 NP) and the final push.
         unsigned b_S = b_size, b_S0 = b_size;   // ring + held; the accounting base (moves with the cellar)
-        unsigned long long b_am = 0;
-        double ca = 0.0, cb = 0.0, cfa = 0.0, cfm = 0.0, cfb = 0.0, cdw = 0.0;   // the held pair (cdw: the dt word)
+        // the held pairs, NP per lane (cdw: the dt word); b_am[p]: the lanes that hold pair p
+        unsigned long long b_am[NP];
+        double ca[NP], cb[NP], cfa[NP], cfm[NP], cfb[NP], cdw[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            b_am[q] = 0;
+            ca[q] = cb[q] = cfa[q] = cfm[q] = cfb[q] = cdw[q] = 0.0;
+        }
         unsigned b_lo1, b_span;
         auto window = [&]() {
             b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : (b_ctop > 0u ? (unsigned)PF_ISSUE : 0u)) + 1u;
-            b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
+            b_span = (unsigned)HI + 1u - b_lo1;
         };
         window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
@@ -1419,64 +1439,96 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             unsigned long long c0 = 0, c1 = 0;
             if constexpr (DIAG) c0 = clk();
             asm volatile("s_setprio 3");
-            // ---- fill: the idle lanes take the ring's top k pairs (rank j among the idle lanes)
-            const unsigned long long need = ~b_am;
-            const unsigned k = min((unsigned)__popcll(need), b_top - b_bot);
-            const unsigned jr = mbcnt(need);
-            const unsigned long long fmsk = __ballot(jr < k) & need;
+            // ---- fill: the idle pair slots take the ring's top k pairs (rank among the idle slots: slot
+            //      0's idle lanes first, then slot 1's)
+            unsigned long long need[NP];
+            unsigned nbase[NP], ntot = 0;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                need[q] = ~b_am[q];
+                nbase[q] = ntot;
+                ntot += (unsigned)__popcll(need[q]);
+            }
+            const unsigned k = min(ntot, b_top - b_bot);
             b_top -= k;
-            const unsigned paddr = ring_addr(ring8, ring_slot(b_top) + jr, ring_vmask);
-            lds_pop6_masked(fmsk, paddr, paddr + 3u * 50u * 512u, ca, cb, cfa, cfm, cfb, cdw);
-            const unsigned long long am = b_am | fmsk;
-            const unsigned na = (unsigned)__popcll(am);
-            const double pa = ca, pb = cb, pfa = cfa, pfm = cfm, pfb = cfb;
-            const unsigned long long dtw = (unsigned long long)__double_as_longlong(cdw);
-            const unsigned dt = (unsigned)dtw;
-            Step2 st[2];
-            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
-            // sign test of the pair word)
-            unsigned long long nospan = 0ull;
-            if constexpr (FID == F_COSH4) nospan = __ballot((int)dt >= 0);
-            double pm, hm;
-            pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+            const unsigned rs = ring_slot(b_top);
+            unsigned long long am[NP];
+            unsigned na = 0;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const unsigned jr = nbase[q] + mbcnt(need[q]);
+                const unsigned long long fmsk = __ballot(jr < k) & need[q];
+                const unsigned paddr = ring_addr(ring8, rs + jr, ring_vmask);
+                lds_pop6_masked(fmsk, paddr, paddr + 3u * 50u * 512u, ca[q], cb[q], cfa[q], cfm[q], cfb[q], cdw[q]);
+                am[q] = b_am[q] | fmsk;
+                na += (unsigned)__popcll(am[q]);
+            }
+            unsigned long long dtw[NP];
+            unsigned dt[NP];
+            unsigned long long nospan = 0ull;   // lanes with a pair lacking SPAN_BIT (one sign test each)
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                dtw[q] = (unsigned long long)__double_as_longlong(cdw[q]);
+                dt[q] = (unsigned)dtw[q];
+                if constexpr (FID == F_COSH4) nospan |= __ballot((int)dt[q] >= 0) & am[q];
+            }
+            Step2 st[2 * NP];
+            double hm[NP];
+            pair_step_halves_n<FID, NP>(ca, cb, cfa, cfm, cfb, eps2, tab, st, hm, kk, FID == F_COSH4 ? 2 : -1, nospan);
             asm volatile("s_setprio 0");
-            const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
-            unsigned long long okm = am;
-            if constexpr (!burst_cap) {
-                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
-                okm = am & dm;
-                const unsigned long long atcap = am & ~dm;
-                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
-            }
-            const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
             b_n += na;   // tasks 2 na; accepted: once per burst from the growth of S (below)
-            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-            const unsigned long long cdtw = dtw + 1ull;   // depth + 1, same integral
-            const unsigned cdt = (unsigned)cdtw;
-            masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
-                        burst_cap ? (mask0 | mask1) : am);
-            if constexpr (DIAG) {
-                const int rtag = (int)dt_tag(dt);
-                b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
-            }
-            if (HIST) {
-                const unsigned d = dt & 255u;
-                if (__builtin_amdgcn_inverse_ballot_w64(am)) {
-                    atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
-                    const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
-                    if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+            unsigned long long mask0[NP], mask1[NP];
+            unsigned long long cdtw[NP];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const unsigned long long r0m = __ballot(st[2 * q].refine), r1m = __ballot(st[2 * q + 1].refine);
+                unsigned long long okm = am[q];
+                if constexpr (!burst_cap) {
+                    const unsigned long long dm = __ballot((dt[q] & 255u) < (unsigned)(max_depth - 1));
+                    okm = am[q] & dm;
+                    const unsigned long long atcap = am[q] & ~dm;
+                    if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
+                }
+                const unsigned long long l0m = am[q] & ~r0m, l1m = am[q] & ~r1m;
+                mask0[q] = okm & r0m;
+                mask1[q] = okm & r1m;
+                cdtw[q] = dtw[q] + 1ull;   // depth + 1, same integral
+                const unsigned cdt = (unsigned)cdtw[q];
+                masked_acc3(acc.r, st[2 * q].area2, l0m, st[2 * q + 1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt[q],
+                            burst_cap ? (mask0[q] | mask1[q]) : am[q]);
+                if constexpr (DIAG) {
+                    const int rtag = (int)dt_tag(dt[q]);
+                    b_mixed |= (__ballot(rtag != tag) & am[q]) != 0ull;
+                }
+                if (HIST) {
+                    const unsigned d = dt[q] & 255u;
+                    if (__builtin_amdgcn_inverse_ballot_w64(am[q])) {
+                        atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                        const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
+                        if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
+                    }
                 }
             }
             if constexpr (DIAG) c1 = clk();
             // ---- task 1's children [m, b] go on the ring (:192-197); task 0's [a, m] stay in the lane
-            lds_push6_masked(mask1, ring_addr(ring8, ring_slot(b_top) + mbcnt(mask1), ring_vmask), hm, pb, pfm,
-                             st[1].fmid, pfb, __longlong_as_double((long long)cdtw));
-            b_top += (unsigned)__popcll(mask1);
-            cb = hm;
-            cfb = pfm;
-            cfm = st[0].fmid;
-            cdw = __longlong_as_double((long long)cdtw);
-            b_am = mask0;
+            const unsigned ps = ring_slot(b_top);
+            unsigned pbase = 0, nkeep = 0;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                lds_push6_masked(mask1[q], ring_addr(ring8, ps + pbase + mbcnt(mask1[q]), ring_vmask), hm[q], cb[q],
+                                 cfm[q], st[2 * q + 1].fmid, cfb[q], __longlong_as_double((long long)cdtw[q]));
+                pbase += (unsigned)__popcll(mask1[q]);
+                nkeep += (unsigned)__popcll(mask0[q]);
+            }
+            b_top += pbase;
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                cb[q] = hm[q];
+                cfb[q] = cfm[q];
+                cfm[q] = st[2 * q].fmid;
+                cdw[q] = __longlong_as_double((long long)cdtw[q]);
+                b_am[q] = mask0[q];
+            }
             if constexpr (DIAG) {
                 if (lane == 0) {
                     const unsigned long long c2 = clk();
@@ -1489,7 +1541,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     atomicAdd(&s_dg[DG_ACTIVE_TASKS], 2ull * na);
                 }
             }
-            b_S = (b_top - b_bot) + (unsigned)__popcll(mask0);
+            b_S = (b_top - b_bot) + nkeep;
             --b_rem;
             unsigned span_r = b_rem != 0u ? b_span : 0u;
             asm("" : "+s"(span_r));
@@ -1501,10 +1553,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             asm volatile("" : "+s"(b_re));
             const unsigned sz = b_S;
             if (b_re != 0u && sz != 0u) {
-                // a cellar edge: S > WCAP - 64 leaves >= WCAP - 128 >= SPILL pairs in the ring; S <=
-                // PF_BELOW leaves the ring room for the landing
-                if (sz > (unsigned)(WCAP - 64)) {
-                    if (b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
+                // a cellar edge: the spill needs SPILL pairs in the ring (always with one held pair per
+                // lane: S > WCAP - 64 leaves >= WCAP - 128; with two the burst ends instead, and the
+                // final push fits: S <= HI + 64 NP = WCAP); S <= PF_BELOW leaves room for the landing
+                if (sz > (unsigned)HI) {
+                    // down to the window again (a round adds up to 64 NP pairs: with two held pairs per lane
+                    // one chunk may not do), or the burst ends and the outer loop spills the rest
+                    while (b_S > (unsigned)HI && b_ctop + (unsigned)SPILL <= (unsigned)CCAP &&
+                           b_top - b_bot >= (unsigned)SPILL) {
                         if (b_pf) {
                             b_ctop += b_pf;
                             b_pf = 0;
@@ -1514,8 +1570,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         b_bot += (unsigned)SPILL;
                         b_S -= (unsigned)SPILL;
                         b_S0 -= (unsigned)SPILL;
-                        b_go = true;
                     }
+                    b_go = b_S <= (unsigned)HI;
                 } else if (b_pf) {
                     if (b_bot < 64u) {
                         b_bot += (unsigned)WCAP;
@@ -1540,9 +1596,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (!b_go) break;
         }
         // the held pairs back on top of the ring
-        lds_push6_masked(b_am, ring_addr(ring8, ring_slot(b_top) + mbcnt(b_am), ring_vmask), ca, cb, cfa, cfm, cfb,
-                         cdw);
-        b_top += (unsigned)__popcll(b_am);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            lds_push6_masked(b_am[q], ring_addr(ring8, ring_slot(b_top) + mbcnt(b_am[q]), ring_vmask), ca[q], cb[q], cfa[q],
+                             cfm[q], cfb[q], cdw[q]);
+            b_top += (unsigned)__popcll(b_am[q]);
+        }
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;

@@ -18,7 +18,7 @@ run() {   # name seconds command...
 for step in "$@"; do
   case $step in
     tests)   run gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
-    ubench)  run ubench_launch 60 tools/ubench_launch && run ubench_step 120 tools/ubench_step ;;
+    ubench)  run ubench_launch 60 tools/ubench_launch && run ubench_step 120 tools/ubench_step && run ubench_step2 180 tools/ubench_step2 ;;
     ab)      ROUNDS=${ROUNDS:-3} AB_GLOB=${AB_GLOB_K:-libaquad_*.so} run ab 900 bash tools/ab.sh "$TAG" ;;
     front)   AB_GLOB=${AB_GLOB_F:-libaquad_*.so} run front 900 bash tools/frontier_ab.sh "$TAG" ;;
     bench)   run bench 400 python bench.py ;;

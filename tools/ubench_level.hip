@@ -114,6 +114,19 @@ __global__ __launch_bounds__(256) void k_copy(const Rec* __restrict__ in, unsign
     }
 }
 
+// The copy at the part's streaming rate: 16 B per lane per access, a grid-stride loop
+// over a grid sized for the 256 CUs (4 workgroups of 256 per CU), non-temporal stores -- the same 1:2
+// read:write shape (every 16-B piece of the input is written twice, to two output halves)
+typedef double d2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_copy4(const d2* __restrict__ in, size_t n16, d2* __restrict__ out) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
+        const d2 v = __builtin_nontemporal_load(in + i);
+        __builtin_nontemporal_store(v, out + i);
+        __builtin_nontemporal_store(v, out + n16 + i);
+    }
+}
+
 // write-only and read-only passes of the same sizes
 __global__ __launch_bounds__(256) void k_write(Rec* __restrict__ out, unsigned n_out) {
     const unsigned i = blockIdx.x * 256 + threadIdx.x;
@@ -187,6 +200,28 @@ int main() {
     if (timeit("nostore", [&] { hipLaunchKernelGGL((k_lvl<true, false>), dim3(grid), dim3(T), 0, 0, din, n, dout, dn, eps, dparts, dtab); })) return 1;
     if (timeit("neither", [&] { hipLaunchKernelGGL((k_lvl<false, false>), dim3(grid), dim3(T), 0, 0, din, n, dout, dn, eps, dparts, dtab); })) return 1;
     if (timeit("copy", [&] { hipLaunchKernelGGL(k_copy, dim3((n + 255) / 256), dim3(256), 0, 0, din, n, dout, refined_children); })) return 1;
+    // the streaming copy at the level's size and at 10x (launch ramp < 10 %): bytes = read + 2 x read
+    for (size_t mult : {(size_t)1, (size_t)10}) {
+        const size_t n16 = (size_t)n * 2 * mult;   // 16-B pieces of the input (32 B per record)
+        d2 *ci, *co;
+        CHECK(hipMalloc(&ci, n16 * 16));
+        CHECK(hipMalloc(&co, 2 * n16 * 16));
+        CHECK(hipMemset(ci, 0, n16 * 16));
+        std::vector<float> t;
+        for (int rep = 0; rep < 12; ++rep) {
+            CHECK(hipEventRecord(a));
+            hipLaunchKernelGGL(k_copy4, dim3(1024), dim3(256), 0, 0, ci, n16, co);
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms; CHECK(hipEventElapsedTime(&ms, a, b)); t.push_back(ms * 1e3f);
+        }
+        std::sort(t.begin(), t.end());
+        const double bytes = 3.0 * 16.0 * (double)n16;
+        printf("{\"variant\": \"copy16_nt_x%zu\", \"bytes\": %.0f, \"us_median\": %.2f, \"us_min\": %.2f, \"GBps_median\": %.1f}\n",
+               mult, bytes, t[6], t[0], bytes / (t[6] * 1e-6) / 1e9);
+        CHECK(hipFree(ci));
+        CHECK(hipFree(co));
+    }
     // (alg_GBps below counts the copy's bytes; the pure passes move only their own)
     {
         std::vector<float> t;
