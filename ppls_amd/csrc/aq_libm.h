@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "aq_exp_table.h"
 #include "aq_sincos_table.h"
 
 #pragma clang fp contract(off)
@@ -32,6 +33,10 @@ struct ExpPair {
     uint64_t tail_bits;
     uint64_t sbits;
 };
+// The exp table in the code object: k_stream's prologue loads it at entry, with no wait for the
+// kernel arguments first (a pointer argument put the argument fetch and the table fetch in series
+// at every launch).
+static __constant__ uint64_t kExpTabBits[256] = {AQ_EXP_TAB_INIT};
 
 // One entry of the LDS copy (stage_exp_table): the same pair, 16-B aligned for one ds_read_b128.
 // (r02 A/B, tools/ab.sh: a 32-B entry that also carried 2^(-j/128)'s high word, so that cosh's first

@@ -127,6 +127,21 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #ifndef AQ_LEAD_SLEEP
 #define AQ_LEAD_SLEEP 2     // s_sleep units (64 clocks) between a waiting leader's polls
 #endif
+// AQ_STAMPS=1 (diagnostic builds only, tools/stamps_single.py): every wave of the plain instance
+// keeps the 100 MHz realtime clock at a few points of its life in registers and stores them once at
+// its exit (g_aq_stamps, read back by aq_debug_stamps) -- the lone launch's timeline without the DIAG
+// instance's LDS atomics
+#ifndef AQ_STAMPS
+#define AQ_STAMPS 0
+#endif
+// AQ_IDLE_FAST: a wave with nothing left counts itself idle with one LDS atomic instead of under
+// the pool lock (only the wave completing the count takes the lock, for the lead check)
+#ifndef AQ_IDLE_FAST
+#define AQ_IDLE_FAST 0
+#endif
+constexpr bool IDLE_FAST = AQ_IDLE_FAST != 0;
+enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
+             ST_XCC, ST_N, ST_STRIDE = 16 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from one integral to the next
@@ -357,7 +372,6 @@ struct StreamParams {
     Chunk* chunks;
     Cellar* cellar;                 // [gridDim.x * NW]
     unsigned* ready;
-    const ExpPair* gtab;
     LaunchHint* hint;
     int per_cu;                     // also keep per-workgroup partials (per-CU task counts; lone integrals)
     int static_jobs;                // fewer than STATIC_MAXK integrals: static job stride (see k_stream)
@@ -616,6 +630,10 @@ __device__ __forceinline__ unsigned ring_wrap(unsigned v) {
 // PCU: the per-CU instance (launches of < PCU_MAXK integrals, P.per_cu): workgroup counts per
 // integral in LDS, folded into the slot sums once at exit -- a lone integral's 3072 waves would
 // otherwise queue on one slot's atomics at every flush.
+#if AQ_STAMPS
+__device__ unsigned long long g_aq_stamps[MAXG * NW * ST_STRIDE];
+#endif
+
 template <int FID, bool HIST, bool DIAG, bool PCU>
 __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // one SoA block (a | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
@@ -644,12 +662,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     QCtl* __restrict__ qc = P.q;
     const LdsPairs R{s_a, s_b, s_fa, s_fm, s_fb, s_dt};
     const unsigned pr_base = (unsigned)(uintptr_t)s_pr;   // LDS byte offset of the pair block (low word of its flat address)
-    const unsigned long long t_entry = DIAG ? rtc() : 0ull;
+    const unsigned long long t_entry = (DIAG || AQ_STAMPS) ? rtc() : 0ull;
+    unsigned long long stp[ST_N] = {};   // AQ_STAMPS: this wave's timeline (wave-uniform)
+    auto stamp = [&](int k) {
+        if constexpr (AQ_STAMPS && !DIAG) { if (!stp[k]) stp[k] = rtc(); }
+    };
+    stp[ST_ENTRY] = t_entry;
     // the exp table's global loads go out first and land in LDS after the other set-up stores (the
     // rings' harmless pairs among them): their latency, a cold HBM read at every launch, overlaps
     // the set-up instead of preceding it
     ExpPair tv{};
-    if (FID != F_SIN_RECIP && tid < 128u) tv = P.gtab[tid];
+    if (FID != F_SIN_RECIP && tid < 128u) tv = reinterpret_cast<const ExpPair*>(kExpTabBits)[tid];
     static_assert(AQ_SINCOS_TAB_N <= PT, "one sin-table entry per thread");
     double sv = 0.0;
     if (FID == F_SIN_RECIP && tid < (unsigned)AQ_SINCOS_TAB_N) sv = kSinCosTab[tid];
@@ -680,6 +703,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     }
     __syncthreads();   // the only workgroup barrier before the exit
     if constexpr (DIAG) { if (tid == 0) s_dg[DG_T_INIT] = rtc(); }
+    stamp(ST_INIT);
 
     const double eps = P.eps;
     const double eps2 = eps / area_scale<FID>();   // the rounds compare doubled areas of f_scale F (task_step_k)
@@ -847,9 +871,24 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             int phase = 0;
             // a wave's first job needs no look at the pool (empty until some wave has run rounds):
             // 12 waves would otherwise queue on the lock before their first F evaluation
+            bool counted_now = false;   // counted idle just now, without the lock, and not the last
             if (fresh && job < total_jobs) {
                 seed = true;
-            } else {
+            } else if (IDLE_FAST && !counted_idle && !job_pending && job >= total_jobs &&
+                       uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                           uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+                // nothing to seed, pool empty: count idle with one LDS atomic. Only the wave that makes
+                // the count whole takes the lock (the lead check below, pool re-read under it); the
+                // others go straight to the lock-free idle poll -- a workgroup's 12 waves running dry
+                // together had queued on the lock one after another
+                stamp(ST_IDLE);
+                unsigned old = 0;
+                if (lane == 0) old = __hip_atomic_fetch_add(&S.idle, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = uni(__shfl(old, 0, 64));
+                counted_idle = true;
+                counted_now = old + 1u != (unsigned)NW;
+            }
+            if (!seed && !counted_now) {
                 wave_lock(&S.lock, lane, lock_spins);
                 {
                     const unsigned avail = uni(S.ptop - S.pbot);
@@ -872,7 +911,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         for (unsigned i = lane; i < k; i += 64) copy_pair(R, POOL0 + ((pb + i) & (PCAP - 1)), base + i);
                         if (lane == 0) {
                             S.pbot = pb + k;
-                            if (counted_idle) S.idle -= 1;
+                            if (counted_idle) __hip_atomic_fetch_add(&S.idle, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                         __builtin_amdgcn_wave_barrier();
                         counted_idle = false;
@@ -880,12 +919,13 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         seed = true;
                     } else {
                         if (!counted_idle) {
-                            if (lane == 0) S.idle += 1;
+                            stamp(ST_IDLE);
+                            if (lane == 0) __hip_atomic_fetch_add(&S.idle, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                             __builtin_amdgcn_wave_barrier();
                             counted_idle = true;
                         }
                         __builtin_amdgcn_wave_barrier();
-                        if (phase == 0 && uni(S.idle) == NW) {   // every wave idle, pool empty, nothing to seed
+                        if (phase == 0 && uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == NW) {   // every wave idle, pool empty, nothing to seed
                             lead = true;
                             if (lane == 0) S.phase = 1;
                             __builtin_amdgcn_wave_barrier();
@@ -915,6 +955,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (seed) {
                 // ---- wave-local seeding of job `job` (see the file header)
                 unsigned long long cs = 0;
+                stamp(ST_SEED_IN);
                 if constexpr (DIAG) {
                     cs = clk();
                     if (lane == 0) atomicMax(&s_dg[DG_T_SEED_IN], rtc());
@@ -1146,6 +1187,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
                 bot = 0;
                 top = (unsigned)__popcll(am);
+                stamp(ST_SEEDED);
                 if constexpr (DIAG) {
                     if (lane == 0) {
                         atomicAdd(&s_dg[DG_SEED_CALLS], 1ull);
@@ -1169,6 +1211,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             // ---- leader: this workgroup has no work; hand its token back and wait for a chunk
             unsigned long long tl = DIAG ? rtc() : 0ull;
+            stamp(ST_LEAD);
             if constexpr (DIAG) {
                 if (lane == 0) {
                     atomicMin(&s_dg[DG_T_FIRST_LEAD], tl);
@@ -1245,7 +1288,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 S.ptop = pt + cnt;
                 S.phase = 0;
                 S.busy_token = 1;
-                S.idle -= 1;   // the leader un-counts itself, so an empty chunk leads to a new leader
+                __hip_atomic_fetch_add(&S.idle, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // the leader un-counts itself, so an empty chunk leads to a new leader
                 // busy again: the group's token comes back if the group was all-idle; the chunk's
                 // cnt + 1 tokens go (one atomic, so T never shows the chunk gone before the group back)
                 const bool was_all_idle = g_add(&qc->idle[grp].v, ~0u) == grp_size;
@@ -1633,8 +1676,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
     if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_BROKE], rtc()); }
+    stamp(ST_BROKE);
     flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
     if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_FLUSHED], rtc()); }
+    stamp(ST_FLUSHED);
     if (mixed) err |= ERRB_OVERFLOW;
     const unsigned werr = wave_or_full(err);
     unsigned last_u = 0;
@@ -1706,6 +1751,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
         }
     }
+#if AQ_STAMPS
+    if constexpr (!DIAG) {
+        stamp(ST_EXIT);
+        stp[ST_XCC] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+        if (lane < (unsigned)ST_N) {   // vector stores, one word per lane
+            unsigned long long v = 0;
+            for (int i = 0; i < ST_N; ++i) v = lane == (unsigned)i ? stp[i] : v;
+            g_aq_stamps[(size_t)(bid * (unsigned)NW + wid) * ST_STRIDE + lane] = v;
+        }
+    }
+#endif
     if constexpr (DIAG) {
         __syncthreads();
         if (tid == 0) {

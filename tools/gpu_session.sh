@@ -30,6 +30,8 @@ for step in "$@"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     xcd)     run xcd_start 120 python tools/xcd_start.py ;;
     ulevel)  run ubench_level 120 tools/ubench_level ;;
+    stamps)  for so in ppls_amd/_build/libaquad_stamps*.so; do n=$(basename $so .so); AQ_LIB=$PWD/$so run ${n#libaquad_} 120 python tools/stamps_single.py; done ;;
+    icache)  run ubench_icache 120 tools/ubench_icache "$OUT/ubench_icache.jsonl" ;;
     pmc)     run pmc 500 bash tools/pmc_profile.sh "pmc_$TAG" ;;
     tests_t) AQ_LIB=$PWD/ppls_amd/_build/libaquad_t_tuned.so run gpu_tests_tuned 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     tests_v) AQ_LIB=$PWD/ppls_amd/_build/${TEST_LIB:?} run gpu_tests_${TEST_LIB%.so} 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
