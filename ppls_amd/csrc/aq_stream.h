@@ -91,6 +91,22 @@ constexpr int JOB_RUN_MAX = AQ_JOB_RUN_MAX;   // most jobs one claim takes (whol
 __host__ __device__ constexpr int seed_depth(unsigned long long V) {
     return V <= 1ull ? AQ_S_W1 : 63 - __builtin_clzll(V) + S_W;
 }
+// positions per share, ceil(2^D / V), for D = seed_depth(V) -- in (2^(S_W-1), 2^S_W] when V > 1, so a
+// count-down of at most 2^(S_W-1) steps instead of a 64-bit division (cold code at every seeding)
+__host__ __device__ constexpr unsigned seed_nb(int D, unsigned long long V) {
+    if (V <= 1ull) return 1u << D;
+    unsigned nb = 1u << S_W;
+    while (nb > 1u && (unsigned long long)(nb - 1u) * V >= (1ull << D)) --nb;
+    return nb;
+}
+// q / nb for small q (seeding's lane -> node map): the float estimate q * rcp(nb), then one
+// correction each way (exact whenever the estimate is off by at most one)
+__device__ __forceinline__ unsigned div_small(unsigned q, unsigned nb, float rnb) {
+    unsigned d = (unsigned)((float)q * rnb);
+    d += (d + 1u) * nb <= q ? 1u : 0u;
+    d -= d * nb > q ? 1u : 0u;
+    return d;
+}
 #ifndef AQ_GIVE_MIN
 #define AQ_GIVE_MIN 96
 #endif
@@ -711,7 +727,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
     unsigned shares_main = (unsigned)P.shares;
     int D_main = P.D;
-    if (P.adaptive & 1) {
+    if (!PCU && (P.adaptive & 1)) {   // (per-CU launches, k < PCU_MAXK, are never adaptive)
         const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
             shares_main = h;
@@ -728,7 +744,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // shares: the jobs the waves draw last are short, so the waves run dry together instead of
     // idling behind the longest last job (each integral keeps ONE partition: the counts are exact)
     // (only where an integral is already several jobs: whole-integral jobs of tiny trees are short)
-    const unsigned tail_from = shares_main >= 8u ? (unsigned)P.tail_from : (unsigned)P.nprob;
+    // (per-CU launches have no tail: k < 64)
+    const unsigned tail_from = (!PCU && shares_main >= 8u) ? (unsigned)P.tail_from : (unsigned)P.nprob;
     const unsigned shares_tail = min(shares_main * (unsigned)P.tail_mult, W);
     const int D_tail = seed_depth((unsigned long long)shares_tail * (unsigned long long)P.nshards);
     const unsigned main_jobs = tail_from * shares_main;
@@ -965,22 +982,30 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const unsigned shares = in_tail ? shares_tail : shares_main;
                 const int D = in_tail ? D_tail : D_main;
                 const unsigned jj = in_tail ? job - main_jobs : job;
-                const int p = (int)((in_tail ? tail_from : 0u) + jj / shares);
+                // (per-CU launches: jobs < PCU_MAXK x W, so the float estimate with its correction
+                // stands in for the integer divisions -- cold code at every lone launch)
+                const float sh_rcp = PCU ? __builtin_amdgcn_rcpf((float)shares) : 0.0f;
+                const unsigned pj = PCU ? div_small(jj, shares, sh_rcp) : jj / shares;
+                const int p = (int)((in_tail ? tail_from : 0u) + pj);
                 const unsigned shard_p = P.shard_of ? (unsigned)uni(P.shard_of[p]) : (unsigned)P.shard;
-                unsigned sh = jj % shares;
+                unsigned sh = jj - pj * shares;
                 // static-job launches rotate the shares from one integral to the next: a wave whose
                 // share of one integral is costly gets another part of the next
-                if (static_jobs) sh = (sh + (unsigned)p * SHARE_ROT) % shares;
+                if (static_jobs) {
+                    const unsigned x = sh + (unsigned)p * SHARE_ROT;
+                    sh = PCU ? x - div_small(x, shares, sh_rcp) * shares : x % shares;
+                }
                 const unsigned vw = sh * (unsigned)P.nshards + shard_p;
                 const unsigned V = shares * (unsigned)P.nshards;
                 const unsigned long long npos_total = 1ull << D;
-                const unsigned nb = (unsigned)((npos_total + V - 1) / V);   // positions per share (<= 8)
+                const unsigned nb = seed_nb(D, V);                          // positions per share (<= 8)
+                const float nb_rcp = __builtin_amdgcn_rcpf((float)nb);      // div_small's estimate
                 const unsigned nlev = (unsigned)D + 1u;                     // seeding evaluates depths 0..D
                 const unsigned nnodes = nlev * nb;
                 // fast path (nnodes <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
                 unsigned long long colmask = 0;
                 if (nnodes <= 64) {
-                    const unsigned kk = lane % nb;
+                    const unsigned kk = lane - div_small(lane, nb, nb_rcp) * nb;
                     for (unsigned d = 0; d < nlev; ++d)
                         if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
                 }
@@ -1036,7 +1061,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     const unsigned q = lane;
                     const bool isnode = q < nnodes;
-                    const unsigned d = isnode ? q / nb : 0u, kk = isnode ? q - d * nb : 0u;
+                    const unsigned d = isnode ? div_small(q, nb, nb_rcp) : 0u, kk = isnode ? q - d * nb : 0u;
                     bool valid = false;
                     const unsigned long long pp = isnode ? position(kk, valid) : 0ull;
                     const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
@@ -1722,7 +1747,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (bid == 0) P.ctls[P.first_slot + p].sums.pcu = 1u;
             }
         }
-        if (last && (P.adaptive & 2)) {
+        if (!PCU && last && (P.adaptive & 2)) {
             const unsigned long long wt = __hip_atomic_load(&S.tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&P.hint->tasks, wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned g = __hip_atomic_fetch_add(&P.hint->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
