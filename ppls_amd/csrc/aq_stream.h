@@ -156,6 +156,15 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #define AQ_IDLE_FAST 0
 #endif
 constexpr bool IDLE_FAST = AQ_IDLE_FAST != 0;
+// AQ_SEED_X (0..2): the seeding pass also evaluates up to X levels below each live position (its
+// children and grandchildren, in the lanes the path nodes leave free), so a job starts with up to
+// 4x more pairs and skips that many half-empty ramp rounds. Same partition (a position's subtree
+// stays with its share), same decisions (the reference's formulas on the same F values).
+#ifndef AQ_SEED_X
+#define AQ_SEED_X 0
+#endif
+constexpr int SEED_X = AQ_SEED_X;
+static_assert(SEED_X >= 0 && SEED_X <= 2, "AQ_SEED_X: 0, 1 or 2 extra seeding levels");
 enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
              ST_XCC, ST_N, ST_STRIDE = 16 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
@@ -1002,6 +1011,17 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const float nb_rcp = __builtin_amdgcn_rcpf((float)nb);      // div_small's estimate
                 const unsigned nlev = (unsigned)D + 1u;                     // seeding evaluates depths 0..D
                 const unsigned nnodes = nlev * nb;
+                // extra levels below the live positions (SEED_X): as many as fit in one wave's lanes
+                // after the path nodes and the two endpoints, and only where no node of them can
+                // reach the depth cap (the path nodes keep the cap's checks)
+                unsigned X = 0;
+                if constexpr (SEED_X > 0) {
+                    if ((int)D + SEED_X + 1 < max_depth) {
+                        if (SEED_X >= 2 && nnodes + 2u + 6u * nb <= 64u) X = 2;
+                        else if (nnodes + 2u + 2u * nb <= 64u) X = 1;
+                    }
+                }
+                const unsigned dt_seed = (unsigned)D + 1u + X;                // depth of the seeds' children
                 // fast path (nnodes <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
                 unsigned long long colmask = 0;
                 if (nnodes <= 64) {
@@ -1061,21 +1081,37 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     const unsigned q = lane;
                     const bool isnode = q < nnodes;
-                    const unsigned d = isnode ? div_small(q, nb, nb_rcp) : 0u, kk = isnode ? q - d * nb : 0u;
+                    // extra lanes (X > 0): from xb on, the live positions' children (kk, c), then
+                    // their grandchildren (kk, g): depth D + xlev, path bits xbits below the position
+                    const unsigned xb = nnodes + 2u;
+                    const unsigned ne1 = X >= 1u ? 2u * nb : 0u, ne2 = X >= 2u ? 4u * nb : 0u;
+                    const bool isx = SEED_X > 0 && q >= xb && q < xb + ne1 + ne2;
+                    const bool isx2 = isx && q >= xb + ne1;
+                    const unsigned xe = isx2 ? q - xb - ne1 : q - xb;
+                    const unsigned xlev = isx ? (isx2 ? 2u : 1u) : 0u;
+                    const unsigned xbits = isx ? (isx2 ? (xe & 3u) : (xe & 1u)) : 0u;
+                    const unsigned d = isnode ? div_small(q, nb, nb_rcp) : (isx ? (unsigned)D + xlev : 0u);
+                    const unsigned kk = isnode ? q - d * nb : (isx ? (isx2 ? xe >> 2 : xe >> 1) : 0u);
                     bool valid = false;
-                    const unsigned long long pp = isnode ? position(kk, valid) : 0ull;
-                    const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
+                    const unsigned long long pp = (isnode || isx) ? position(kk, valid) : 0ull;
+                    const unsigned long long anc = !valid ? 0ull
+                                                  : isx ? ((pp << xlev) | (unsigned long long)xbits)
+                                                        : (pp >> (D - (int)d));
                     unsigned li = nnodes, ri = nnodes + 1;
                     for (unsigned i = 0; i < d; ++i) {
                         const double mm = (l + r) / 2;
-                        if ((anc >> (d - 1 - i)) & 1ull) { l = mm; li = i * nb + kk; } else { r = mm; ri = i * nb + kk; }
+                        // the node whose midpoint this step's new endpoint is: path node (i, kk), or
+                        // for a grandchild's last step its parent child (kk, c)
+                        const unsigned ia = (SEED_X == 0 || i < nlev) ? i * nb + kk : xb + 2u * kk + (xbits >> 1);
+                        if ((anc >> (d - 1 - i)) & 1ull) { l = mm; li = ia; } else { r = mm; ri = ia; }
                     }
                     mid = (l + r) / 2;                                        // :187
                     if constexpr (DIAG) { asm volatile("" :: "v"(mid)); cb = clk(); }
-                    const unsigned fq = nnodes + 2 <= 64 ? q : (q < nnodes ? q : 64u);
-                    if (fq < nnodes + 2)
-                        fmid = integrand<FID>(isnode ? mid : (q == nnodes ? A : B), tab);   // :188
-                    if (fq < nnodes + 2) fm[q] = fmid;
+                    const unsigned nev = nnodes + 2u + ne1 + ne2;             // lanes that evaluate F
+                    const unsigned fq = nev <= 64 ? q : (q < nnodes ? q : 64u);
+                    if (fq < nev)
+                        fmid = integrand<FID>((isnode || isx) ? mid : (q == nnodes ? A : B), tab);   // :188
+                    if (fq < nev) fm[q] = fmid;
                     if (nnodes + 2 > 64 && lane < 2) fm[nnodes + lane] = integrand<FID>(lane == 0 ? A : B, tab);
                     if constexpr (DIAG) {
                         cp1 = clk();
@@ -1087,7 +1123,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     bool refine = false;
                     double leafarea = 0.0;
-                    if (isnode) {
+                    if (isnode || isx) {
                         fl = fm[li];
                         fr = fm[ri];
                         const double lrarea = (fl + fr) * (r - l) / 2;        // :185
@@ -1112,8 +1148,30 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     // a surviving position node emits its children pair (depth D + 1)
                     alive = isnode && valid && (int)d == D && dstar >= nlev && D + 1 < max_depth;
+                    if constexpr (SEED_X > 0) {
+                        if (X > 0u) {
+                            // the live positions' children, then grandchildren: each exists when its
+                            // parent refines; every existing one is a task of this share (no shared
+                            // ancestors below a position); the deepest level's refining nodes are the seeds
+                            const unsigned long long am_pos = __ballot(alive);
+                            bool exists = isx && valid && ((am_pos >> (nlev * nb - nb + kk)) & 1ull);
+                            const unsigned long long am_r1 = __ballot(exists && !isx2 && refine);
+                            if (isx2) exists = exists && ((am_r1 >> (xb + 2u * kk + (xbits >> 1))) & 1ull);
+                            if (exists) {
+                                ++acc.tasks;
+                                acc.maxd = max(acc.maxd, d + 1u);
+                                if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
+                                if (!refine) {
+                                    dd_add(acc.hi, acc.lo, leafarea / area_scale<FID>());   // :199 -> :149
+                                    ++acc.leaves;
+                                    if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
+                                }
+                            }
+                            alive = exists && refine && xlev == X;
+                        }
+                    }
                     // (the per-burst cap's maxdt counts pushed pairs only: the seeds' depth goes here)
-                    if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
+                    if (burst_cap && alive) acc.maxd = max(acc.maxd, dt_seed + 1u);
                     if constexpr (DIAG) cp2 = clk();
                 } else {
                     for (unsigned q0 = 0; q0 < nnodes + 2; q0 += 64) {
@@ -1208,7 +1266,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     // a pair holds its endpoints halved (aq_device.h pair_step_halves; exact)
                     s_a[j] = 0.5 * l; s_b[j] = 0.5 * r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
                     const bool span = FID == F_COSH4 && cosh_main_span(l, r);
-                    s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
+                    s_dt[j] = dt_seed | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }
                 bot = 0;
                 top = (unsigned)__popcll(am);
