@@ -156,6 +156,31 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #define AQ_IDLE_FAST 0
 #endif
 constexpr bool IDLE_FAST = AQ_IDLE_FAST != 0;
+// AQ_DONE_GROUPS: the run's end is stored into one flag line per termination group, and a waiting
+// leader polls its group's line -- 32 pollers per line instead of every workgroup's leader on one
+#ifndef AQ_DONE_GROUPS
+#define AQ_DONE_GROUPS 0
+#endif
+constexpr bool DONE_GROUPS = AQ_DONE_GROUPS != 0;
+// AQ_IDLE_FLUSH: a wave flushes its accumulators when it first runs dry, off the run's critical
+// path, instead of every wave at once after the end is seen
+#ifndef AQ_IDLE_FLUSH
+#define AQ_IDLE_FLUSH 0
+#endif
+constexpr bool IDLE_FLUSH = AQ_IDLE_FLUSH != 0;
+// AQ_LAZY_TICKET (per-CU launches): a new leader first polls only the end flag, for up to this many
+// spins, before it takes a queue ticket -- at a lone launch's end 255 leaders drawing tickets from one
+// counter (~12 ns each) held the last of them ~3 us past the end
+#ifndef AQ_LAZY_TICKET
+#define AQ_LAZY_TICKET 0
+#endif
+constexpr unsigned LAZY_TICKET = AQ_LAZY_TICKET;
+// AQ_RING_INIT: fill every ring slot with a harmless pair at entry (18 K LDS stores per CU). The
+// carried round reads ring slots only through masked pops of pairs that were pushed
+#ifndef AQ_RING_INIT
+#define AQ_RING_INIT 1
+#endif
+constexpr bool RING_INIT = AQ_RING_INIT != 0;
 // AQ_SEED_X (0..2): the seeding pass also evaluates up to X levels below each live position (its
 // children and grandchildren, in the lanes the path nodes leave free), so a job starts with up to
 // 4x more pairs and skips that many half-empty ramp rounds. Same partition (a position's subtree
@@ -166,7 +191,7 @@ constexpr bool IDLE_FAST = AQ_IDLE_FAST != 0;
 constexpr int SEED_X = AQ_SEED_X;
 static_assert(SEED_X >= 0 && SEED_X <= 2, "AQ_SEED_X: 0, 1 or 2 extra seeding levels");
 enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
-             ST_XCC, ST_N, ST_STRIDE = 16 };
+             ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_N, ST_STRIDE = 16 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from one integral to the next
@@ -283,6 +308,7 @@ struct QCtl {
     Line jobs;                 // job claims beyond the first W
     Line done;                 // 1: T reached 0, every workgroup exits
     Line idle[NGROUP];         // idle workgroups per group
+    Line done_g[NGROUP];       // AQ_DONE_GROUPS: `done` again, one line per group (its pollers only)
 };
 // Per-integral totals: device-scope atomics at every flush (the farmer's `result += buff[0]`, :149,
 // and tasks_per_process, :162). The area is the exact fixed-point sum of the waves' double-double
@@ -693,6 +719,11 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if constexpr (AQ_STAMPS && !DIAG) { if (!stp[k]) stp[k] = rtc(); }
     };
     stp[ST_ENTRY] = t_entry;
+    if constexpr (AQ_STAMPS && !DIAG) {
+        // the kernel arguments' first arrival (the set-up's and the first seeding's fields)
+        asm volatile("" :: "s"(P.eps), "s"(P.shares), "s"(P.nprob), "s"(P.kbounds[0].x));
+        stamp(ST_KARG);
+    }
     // the exp table's global loads go out first and land in LDS after the other set-up stores (the
     // rings' harmless pairs among them): their latency, a cold HBM read at every launch, overlaps
     // the set-up instead of preceding it
@@ -701,13 +732,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     static_assert(AQ_SINCOS_TAB_N <= PT, "one sin-table entry per thread");
     double sv = 0.0;
     if (FID == F_SIN_RECIP && tid < (unsigned)AQ_SINCOS_TAB_N) sv = kSinCosTab[tid];
-    {
+    if constexpr (RING_INIT) {
         const unsigned b0 = (tid >> 6) * WCAP;
         for (unsigned i = lane_id(); i < (unsigned)WCAP; i += 64) {
             const unsigned j = b0 + i;
             s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
         }
     }
+    stamp(ST_PRE);
     if (bid == 0)
         for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
     if (tid == 0) {
@@ -913,6 +945,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 old = uni(__shfl(old, 0, 64));
                 counted_idle = true;
                 counted_now = old + 1u != (unsigned)NW;
+                // (IDLE_FLUSH: not the workgroup's last: its flush overlaps the others' work; the
+                // last one leads, and flushes behind its first termination atomic)
+                if constexpr (IDLE_FLUSH) { if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px); }
             }
             if (!seed && !counted_now) {
                 wave_lock(&S.lock, lane, lock_spins);
@@ -1059,6 +1094,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     job = total_jobs;
                 }
                 const double A = ab.x, B = ab.y;
+                if constexpr (AQ_STAMPS && !DIAG) { asm volatile("" :: "s"(A)); stamp(ST_CLASS); }
                 double* fm = s_a + base;          // [nnodes + 2]: F(mid of (d,k)) at d*nb+k, then F(A), F(B)
                 double* leafa = s_b + base;       // [nnodes]: larea + rarea of node (d,k)
                 const DtField flag = s_dt + base;  // [nnodes]: node (d,k) refines
@@ -1112,6 +1148,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     if (fq < nev)
                         fmid = integrand<FID>((isnode || isx) ? mid : (q == nnodes ? A : B), tab);   // :188
                     if (fq < nev) fm[q] = fmid;
+                    if constexpr (AQ_STAMPS && !DIAG) { asm volatile("" :: "v"(fmid)); stamp(ST_FEVAL); }
                     if (nnodes + 2 > 64 && lane < 2) fm[nnodes + lane] = integrand<FID>(lane == 0 ? A : B, tab);
                     if constexpr (DIAG) {
                         cp1 = clk();
@@ -1303,27 +1340,46 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             int cmd = -1;   // >= 0 chunk slot, -1 exit, -2 error
             unsigned cnt = 0;
+            unsigned r_idle = 0;
+            bool had_token = false;
+            if (lane == 0) {
+                had_token = S.busy_token != 0;
+                if (had_token) {
+                    S.busy_token = 0;
+                    r_idle = g_add(&qc->idle[grp].v, 1u);
+                }
+            }
+            // (IDLE_FLUSH: the leader's own flush runs while that atomic is in flight)
+            if constexpr (IDLE_FLUSH) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
             if (lane == 0) {
                 bool last = false;   // this workgroup's idle transition ended the run
-                if (S.busy_token) {
-                    S.busy_token = 0;
-                    if (g_add(&qc->idle[grp].v, 1u) + 1u == grp_size)   // the group's last busy workgroup
-                        last = g_add((int*)&qc->tokens.v, -1) - 1 == -t0;
-                }
+                if (had_token && r_idle + 1u == grp_size)   // the group's last busy workgroup
+                    last = g_add((int*)&qc->tokens.v, -1) - 1 == -t0;
                 if (last) {
                     st_wt(&qc->done.v, 1u);
+                    if constexpr (DONE_GROUPS)
+                        for (int g = 0; g < NGROUP; ++g) st_wt(&qc->done_g[g].v, 1u);
                 } else {
-                    const unsigned h = g_add(&qc->head.v, 1u);
+                    // LAZY_TICKET: the end flag alone first (one load per spin, no ticket)
+                    bool ended = false;
+                    if constexpr (PCU && LAZY_TICKET > 0) {
+                        for (unsigned spins = 0; spins < LAZY_TICKET; ++spins) {
+                            if (ld_wt(DONE_GROUPS ? &qc->done_g[grp].v : &qc->done.v)) { ended = true; break; }
+                            __builtin_amdgcn_s_sleep(AQ_LEAD_SLEEP);
+                        }
+                    }
+                    if (ended) cmd = -1;
+                    const unsigned h = ended ? 0u : g_add(&qc->head.v, 1u);
                     // the wait is bounded by time WITHOUT PROGRESS, not since launch: while work exists,
                     // busy waves donate to waiting tickets within POLL_ROUNDS rounds, and every donation
                     // or idle / busy transition moves the token count or the queue tail
                     unsigned long long t_prog = rtc();
                     int seen_tk = 0;
                     unsigned seen_tl = ~0u;
-                    for (unsigned spins = 0;; ++spins) {
+                    for (unsigned spins = 0; !ended; ++spins) {
                         // both words are read every spin, issued together (one latency per spin)
                         const unsigned rv = h < P.qcap ? ld_wt(&P.ready[(size_t)h * READY_STRIDE]) : 0u;
-                        const unsigned dn = ld_wt(&qc->done.v);
+                        const unsigned dn = ld_wt(DONE_GROUPS ? &qc->done_g[grp].v : &qc->done.v);
                         if (rv == P.epoch) { cmd = (int)h; break; }
                         if (dn) { cmd = -1; break; }
                         if ((spins & 63u) == 63u) {
@@ -1351,6 +1407,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             cmd = uni(__shfl(cmd, 0, 64));
             cnt = uni(__shfl(cnt, 0, 64));
             if constexpr (DIAG) { if (lane == 0 && cmd < 0) atomicMax(&s_dg[DG_T_DONE], rtc()); }
+            if (cmd < 0) stamp(ST_DONE);
             if (cmd < 0) {
                 wave_lock(&S.lock, lane, lock_spins);
                 if (lane == 0) S.phase = 2;

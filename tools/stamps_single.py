@@ -2,9 +2,10 @@
 -DAQ_STAMPS=1: python ppls_amd/build.py --variant stamps -DAQ_STAMPS=1, then
 AQ_LIB=$PWD/ppls_amd/_build/libaquad_stamps.so python tools/stamps_single.py).
 
-Every wave keeps the 100 MHz realtime clock at entry, after the workgroup barrier, at its first
-seeding's start and end, when it first counts itself idle, when it first leads, when it leaves the
-loop, after its flush and at its exit (aq_stream.h ST_*). Printed: the quantiles over waves of each
+Every wave keeps the 100 MHz realtime clock at entry, after its ring set-up, after the workgroup
+barrier, at its first seeding's start, bounds, F evaluation and end, when it first counts itself
+idle, when it first leads and sees the end, when it leaves the loop, after its flush and at its
+exit (aq_stream.h ST_*). Printed: the quantiles over waves of each
 point relative to the earliest entry, per tree size, with the kernel's own HIP-event time.
 """
 import argparse
@@ -19,7 +20,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from ppls_amd import Context, Problem  # noqa: E402
 
-NAMES = ["entry", "init", "seed_in", "seeded", "idle", "lead", "broke", "flushed", "exit"]
+# aq_stream.h ST_* order (ST_XCC = 9 holds the XCD id, not a time)
+NAMES = ["entry", "init", "seed_in", "seeded", "idle", "lead", "broke", "flushed", "exit", None,
+         "pre", "class", "feval", "done", "karg"]
+ORDER = ["entry", "karg", "pre", "init", "seed_in", "class", "feval", "seeded", "idle", "lead", "done", "broke",
+         "flushed", "exit"]
 ST_XCC, ST_STRIDE, NW = 9, 16, 12
 
 
@@ -32,7 +37,8 @@ def timeline(ctx, grid):
     a = np.frombuffer(buf, dtype=np.uint64).reshape(grid * NW, ST_STRIDE).astype(np.int64)
     t0 = a[:, 0].min()
     out = {}
-    for i, nm in enumerate(NAMES):
+    for nm in ORDER:
+        i = NAMES.index(nm)
         v = a[:, i]
         v = v[v > 0]
         if len(v) == 0:
@@ -54,7 +60,7 @@ def main():
     ctx.L.aq_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     grid = ctx.num_cus
     res = {"lib": os.environ.get("AQ_LIB", "default"), "grid": grid,
-           "points": NAMES, "format": "us after the earliest wave entry: q0, q50, q90, q100, waves"}
+           "points": ORDER, "format": "us after the earliest wave entry: q0, q50, q90, q100, waves"}
     for name, p in [("one_task", Problem(eps=1e9)), ("eps1e-6", Problem(eps=1e-6)),
                     ("eps1e-10", Problem(eps=1e-10))]:
         ctx.integrate_async(p, 0)
