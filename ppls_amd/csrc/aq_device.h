@@ -184,52 +184,6 @@ __device__ __forceinline__ void pair_step_halves(double ha, double hb, double fa
     }
 }
 
-// NP pairs per lane at once (2 NP tasks, 2 NP interleaved F chains): pair_step_halves' arithmetic
-// for each pair, the F evaluations of all of them in one integrand_k call.
-template <int FID, int NP>
-__device__ __forceinline__ void pair_step_halves_n(const double (&ha)[NP], const double (&hb)[NP], const double (&fa)[NP],
-                                                   const double (&fm)[NP], const double (&fb)[NP], double eps2,
-                                                   const ExpEntry* __restrict__ tab, Step2 (&s)[2 * NP],
-                                                   double (&hm)[NP], const ExpConsts& kk, int range_hint,
-                                                   unsigned long long out_mask) {
-    double mid[2 * NP], lr2e[2 * NP], wl[2 * NP], wr[2 * NP], fl[2 * NP], fr[2 * NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const double m = ha[p] + hb[p];                      // the parent's midpoint (:187)
-        hm[p] = 0.5 * m;
-        mid[2 * p] = ha[p] + hm[p];                          // :187 for [a, m] and [m, b]
-        mid[2 * p + 1] = hm[p] + hb[p];
-        fl[2 * p] = fa[p]; fr[2 * p] = fm[p];
-        fl[2 * p + 1] = fm[p]; fr[2 * p + 1] = fb[p];
-        lr2e[2 * p] = (fa[p] + fm[p]) * __fma_rn(ha[p], -2.0, m);     // (fl + fr) * (r - l), :185
-        lr2e[2 * p + 1] = (fm[p] + fb[p]) * __fma_rn(hb[p], 2.0, -m);
-        wl[2 * p] = __fma_rn(ha[p], -2.0, mid[2 * p]);       // mid - l
-        wl[2 * p + 1] = mid[2 * p + 1] - m;
-        wr[2 * p] = m - mid[2 * p];                          // r - mid
-        wr[2 * p + 1] = __fma_rn(hb[p], 2.0, -mid[2 * p + 1]);
-    }
-#pragma unroll
-    for (int k = 0; k < 2 * NP; ++k) asm volatile("" : "+v"(lr2e[k]), "+v"(wl[k]), "+v"(wr[k]));
-    double fmid[2 * NP];
-    integrand_k<FID, 2 * NP, (f_scale<FID>() != 1.0)>(mid, fmid, tab, kk, range_hint, out_mask);   // :188
-#pragma unroll
-    for (int k = 0; k < 2 * NP; ++k) {
-        s[k].fmid = fmid[k];
-        if constexpr (doubled_areas<FID>()) {
-            const double l2 = (fl[k] + fmid[k]) * wl[k];     // 2 * larea, :189
-            const double r2 = (fmid[k] + fr[k]) * wr[k];     // 2 * rarea, :190
-            s[k].area2 = l2 + r2;
-            s[k].refine = fabs(s[k].area2 - lr2e[k]) > eps2;   // :191 (strict >)
-        } else {
-            const double lrarea = lr2e[k] / 2;                // :185
-            const double larea = (fl[k] + fmid[k]) * wl[k] / 2;   // :189
-            const double rarea = (fmid[k] + fr[k]) * wr[k] / 2;   // :190
-            s[k].area2 = larea + rarea;                       // :199
-            s[k].refine = fabs((larea + rarea) - lrarea) > eps2;   // :191
-        }
-    }
-}
-
 // pair_step_halves with the parent's doubled areas carried in (doubled-area integrands only). A child's
 // lrarea (:185) is token for token its parent's larea / rarea (:189 / :190: the same F values and
 // the same width m - a, b - m), so a pair that carries its parent's two products, lr0 = 2 larea and

@@ -39,15 +39,8 @@ namespace aq {
 
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
-// Pairs each lane carries (AQ_NP): 1 -- 12 waves per CU (3 per SIMD), 2 -- 8 waves per CU (2 per SIMD,
-// four interleaved F chains per lane, the VGPR budget of 2 waves)
-#ifndef AQ_NP
-#define AQ_NP 1
-#endif
-constexpr int NP = AQ_NP;
-static_assert(NP == 1 || NP == 2, "one or two carried pairs per lane");
 #ifndef AQ_PT
-#define AQ_PT (AQ_NP == 1 ? 768 : 512)
+#define AQ_PT 768
 #endif
 #ifndef AQ_WCAP
 #define AQ_WCAP 256
@@ -64,9 +57,7 @@ constexpr int WCAP = AQ_WCAP;       // per-wave LDS ring, pairs: a round pops <=
 // access; the pool went from 256 to 128 pairs to make room).
 constexpr int PCAP = 128;           // per-workgroup LDS pool ring, pairs (power of two)
 constexpr int DT_STRIDE = 2;        // dt words per slot (the low word of an 8-byte field)
-constexpr int LREC = 3200;          // LDS pair slots per field: 3200 x 48 B = 150 KiB (the pair moves' offsets
-                                    // assume it; with 8 waves the rings and pool use 2176 of them)
-static_assert(NW * WCAP + PCAP <= LREC, "the rings and the pool fit the pair block");
+constexpr int LREC = NW * WCAP + PCAP;   // LDS pair slots: 3200 x 48 B = 150 KiB
 constexpr int POOL0 = NW * WCAP;    // first pool slot
 constexpr int CH = PCAP;            // pairs per HBM queue chunk (<= PCAP: a chunk lands in an empty pool)
 // the pair words of the LDS block: slot j's word at p[DT_STRIDE * j]
@@ -150,46 +141,10 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #ifndef AQ_STAMPS
 #define AQ_STAMPS 0
 #endif
-// AQ_IDLE_FAST: a wave with nothing left counts itself idle with one LDS atomic instead of under
-// the pool lock (only the wave completing the count takes the lock, for the lead check)
-#ifndef AQ_IDLE_FAST
-#define AQ_IDLE_FAST 0
-#endif
-constexpr bool IDLE_FAST = AQ_IDLE_FAST != 0;
-// AQ_DONE_GROUPS: the run's end is stored into one flag line per termination group, and a waiting
-// leader polls its group's line -- 32 pollers per line instead of every workgroup's leader on one
-#ifndef AQ_DONE_GROUPS
-#define AQ_DONE_GROUPS 0
-#endif
-constexpr bool DONE_GROUPS = AQ_DONE_GROUPS != 0;
-// AQ_IDLE_FLUSH: a wave flushes its accumulators when it first runs dry, off the run's critical
-// path, instead of every wave at once after the end is seen
-#ifndef AQ_IDLE_FLUSH
-#define AQ_IDLE_FLUSH 0
-#endif
-constexpr bool IDLE_FLUSH = AQ_IDLE_FLUSH != 0;
-// AQ_LAZY_TICKET (per-CU launches): a new leader first polls only the end flag, for up to this many
+// Per-CU (lone) launches: a new leader first polls only its group's end flag, for up to LAZY_TICKET
 // spins, before it takes a queue ticket -- at a lone launch's end 255 leaders drawing tickets from one
-// counter (~12 ns each) held the last of them ~3 us past the end
-#ifndef AQ_LAZY_TICKET
-#define AQ_LAZY_TICKET 0
-#endif
-constexpr unsigned LAZY_TICKET = AQ_LAZY_TICKET;
-// AQ_RING_INIT: fill every ring slot with a harmless pair at entry (18 K LDS stores per CU). The
-// carried round reads ring slots only through masked pops of pairs that were pushed
-#ifndef AQ_RING_INIT
-#define AQ_RING_INIT 1
-#endif
-constexpr bool RING_INIT = AQ_RING_INIT != 0;
-// AQ_SEED_X (0..2): the seeding pass also evaluates up to X levels below each live position (its
-// children and grandchildren, in the lanes the path nodes leave free), so a job starts with up to
-// 4x more pairs and skips that many half-empty ramp rounds. Same partition (a position's subtree
-// stays with its share), same decisions (the reference's formulas on the same F values).
-#ifndef AQ_SEED_X
-#define AQ_SEED_X 0
-#endif
-constexpr int SEED_X = AQ_SEED_X;
-static_assert(SEED_X >= 0 && SEED_X <= 2, "AQ_SEED_X: 0, 1 or 2 extra seeding levels");
+// counter (~12 ns each, MI355X_MICROARCH.md "fanin") held the last of them ~3 us past the end (r04j/k)
+constexpr unsigned LAZY_TICKET = 64;
 enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
              ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_N, ST_STRIDE = 16 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
@@ -216,9 +171,7 @@ static_assert((unsigned)MAXK - 1u <= TAG_MASK, "the tag field must hold every in
 constexpr int NPARTS = 65536;
 __host__ __device__ __forceinline__ size_t parts_row(int slot) { return slot < NPARTS ? (size_t)slot : (size_t)NPARTS; }
 #ifndef AQ_GSPLIT_DEFAULT
-// sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11,
-// 96 -> 1.803e11); a multiple of the waves per workgroup, so that it divides the launch's waves
-#define AQ_GSPLIT_DEFAULT (8 * (AQ_PT / 64))
+#define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
 #ifndef AQ_LONE_GSPLIT
@@ -231,10 +184,7 @@ constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's 
 #endif
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
-// the burst window's top: a round moves at most NP pairs per lane into the ring (and the burst's end
-// the held ones), so S = ring + held <= WCAP - 64 NP at a round's start keeps the ring from overflowing
-constexpr int HI = WCAP - 64 * NP;
-constexpr int REFILL = HI;          // pairs a wave with an empty ring takes back from its cellar
+constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 #ifndef AQ_PF_BELOW
 // r02 A/B (8192-integral launch, GIVE_ROUNDS 32): 112 28.39, 96 27.93, 80 27.57, 64 27.20, 48 28.18,
 // 32 30.25 ms, no prefetch 33.37 ms. The old 128 (= WCAP - 128) made a ring that had just spilled
@@ -250,10 +200,10 @@ constexpr int PF_BELOW = AQ_PF_BELOW;   // below this ring size a wave prefetche
 // 80 % of the prefetches then have >= 2 rounds to arrive instead of 1). A ring that overflows while
 // they are in flight cancels them (the pairs are still in the cellar: only ctop moved) and spills.
 #ifndef AQ_PF_ISSUE
-#define AQ_PF_ISSUE (AQ_NP == 1 ? 160 : 96)   // r03 A/B (8192 x eps=1e-10): 96 -0.6 %, 128 -1.8 %, 160 -2.4 % vs landing after one round
+#define AQ_PF_ISSUE 160   // r03 A/B (8192 x eps=1e-10): 96 -0.6 %, 128 -1.8 %, 160 -2.4 % vs landing after one round
 #endif
 constexpr int PF_ISSUE = AQ_PF_ISSUE;
-static_assert(PF_ISSUE >= PF_BELOW && PF_ISSUE < HI && PF_BELOW + 64 <= HI, "a landed prefetch must leave the ring below the spill line");
+static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed prefetch must leave the ring below the spill line");
 // In-burst cellar moves (r03): a round that leaves the burst's size window at a cellar edge -- above
 // the spill line, or down to the prefetch issue / landing line -- moves the chunk inside the burst
 // and the burst goes on, where round 2 left the burst for the outer loop (~60 VALU and ~70 SALU of
@@ -306,9 +256,9 @@ struct QCtl {
     Line head;                 // tickets taken by idle workgroups
     Line tokens;               // T - T0
     Line jobs;                 // job claims beyond the first W
-    Line done;                 // 1: T reached 0, every workgroup exits
     Line idle[NGROUP];         // idle workgroups per group
-    Line done_g[NGROUP];       // AQ_DONE_GROUPS: `done` again, one line per group (its pollers only)
+    Line done[NGROUP];         // 1: T reached 0, every workgroup exits -- one line per group, polled by
+                               // that group's waiting leaders only (32 pollers per line, not 256)
 };
 // Per-integral totals: device-scope atomics at every flush (the farmer's `result += buff[0]`, :149,
 // and tasks_per_process, :162). The area is the exact fixed-point sum of the waves' double-double
@@ -724,21 +674,15 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         asm volatile("" :: "s"(P.eps), "s"(P.shares), "s"(P.nprob), "s"(P.kbounds[0].x));
         stamp(ST_KARG);
     }
-    // the exp table's global loads go out first and land in LDS after the other set-up stores (the
-    // rings' harmless pairs among them): their latency, a cold HBM read at every launch, overlaps
-    // the set-up instead of preceding it
+    // the exp table's global loads go out first and land in LDS after the other set-up stores: their
+    // latency overlaps the set-up instead of preceding it. (The rings are not pre-filled: the carried
+    // round reads ring slots only through masked pops of pushed pairs -- the fill's 18 K LDS stores per
+    // CU had cost every launch 0.75 us, r04j)
     ExpPair tv{};
     if (FID != F_SIN_RECIP && tid < 128u) tv = reinterpret_cast<const ExpPair*>(kExpTabBits)[tid];
     static_assert(AQ_SINCOS_TAB_N <= PT, "one sin-table entry per thread");
     double sv = 0.0;
     if (FID == F_SIN_RECIP && tid < (unsigned)AQ_SINCOS_TAB_N) sv = kSinCosTab[tid];
-    if constexpr (RING_INIT) {
-        const unsigned b0 = (tid >> 6) * WCAP;
-        for (unsigned i = lane_id(); i < (unsigned)WCAP; i += 64) {
-            const unsigned j = b0 + i;
-            s_a[j] = 1.0; s_b[j] = 1.0; s_fa[j] = 0.0; s_fm[j] = 0.0; s_fb[j] = 0.0; s_dt[j] = 0;
-        }
-    }
     stamp(ST_PRE);
     if (bid == 0)
         for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
@@ -829,6 +773,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // siblings every SKEWED_GIVE rounds (a lone integral 79 -> 70 us at 4; cosh4 keeps 32, where 4 cost
     // the eps=1e-12 lone tree 47 -> 61 us and the bench 0.6 %; profiles/r02_ab/fast_give_poll*.txt)
     // (a faster cadence for lone launches, give every 4 / 8 rounds: slower, profiles/r03zb)
+    // (per-CU launches feeding idle siblings every 4 / 8 / 16 rounds: ε=1e-10 lone 24 -> 35 / 30 / 26 us,
+    // the bursts cut short; r04k)
     constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE : (unsigned)GIVE_ROUNDS;
     constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL : (unsigned)POLL_ROUNDS;
     constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN : (unsigned)GIVE_MIN;
@@ -932,22 +878,19 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             bool counted_now = false;   // counted idle just now, without the lock, and not the last
             if (fresh && job < total_jobs) {
                 seed = true;
-            } else if (IDLE_FAST && !counted_idle && !job_pending && job >= total_jobs &&
+            } else if (!counted_idle && !job_pending && job >= total_jobs &&
                        uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
                            uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
                 // nothing to seed, pool empty: count idle with one LDS atomic. Only the wave that makes
                 // the count whole takes the lock (the lead check below, pool re-read under it); the
                 // others go straight to the lock-free idle poll -- a workgroup's 12 waves running dry
-                // together had queued on the lock one after another
+                // together had queued on the lock one after another (1-task tree 16.4 -> 15.3 us, r04h)
                 stamp(ST_IDLE);
                 unsigned old = 0;
                 if (lane == 0) old = __hip_atomic_fetch_add(&S.idle, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 old = uni(__shfl(old, 0, 64));
                 counted_idle = true;
                 counted_now = old + 1u != (unsigned)NW;
-                // (IDLE_FLUSH: not the workgroup's last: its flush overlaps the others' work; the
-                // last one leads, and flushes behind its first termination atomic)
-                if constexpr (IDLE_FLUSH) { if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px); }
             }
             if (!seed && !counted_now) {
                 wave_lock(&S.lock, lane, lock_spins);
@@ -1046,23 +989,14 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 const float nb_rcp = __builtin_amdgcn_rcpf((float)nb);      // div_small's estimate
                 const unsigned nlev = (unsigned)D + 1u;                     // seeding evaluates depths 0..D
                 const unsigned nnodes = nlev * nb;
-                // extra levels below the live positions (SEED_X): as many as fit in one wave's lanes
-                // after the path nodes and the two endpoints, and only where no node of them can
-                // reach the depth cap (the path nodes keep the cap's checks)
-                unsigned X = 0;
-                if constexpr (SEED_X > 0) {
-                    if ((int)D + SEED_X + 1 < max_depth) {
-                        if (SEED_X >= 2 && nnodes + 2u + 6u * nb <= 64u) X = 2;
-                        else if (nnodes + 2u + 2u * nb <= 64u) X = 1;
-                    }
-                }
-                const unsigned dt_seed = (unsigned)D + 1u + X;                // depth of the seeds' children
                 // fast path (nnodes <= 64): lane q = d*nb + kk; colmask = the lanes of this lane's kk
                 unsigned long long colmask = 0;
                 if (nnodes <= 64) {
-                    const unsigned kk = lane - div_small(lane, nb, nb_rcp) * nb;
-                    for (unsigned d = 0; d < nlev; ++d)
-                        if (d * nb + kk < 64u) colmask |= 1ull << (d * nb + kk);
+                    // column 0's lanes, built once per wave on the scalar unit, shifted to this lane's
+                    // column (a per-lane loop of 64-bit shifts had cost the lone start ~0.3 us)
+                    unsigned long long col0 = 0;
+                    for (unsigned d = 0; d < nlev; ++d) col0 |= 1ull << (d * nb);
+                    colmask = uni(col0) << (lane - div_small(lane, nb, nb_rcp) * nb);
                 }
                 if (p != tag) {
                     flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
@@ -1117,37 +1051,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     const unsigned q = lane;
                     const bool isnode = q < nnodes;
-                    // extra lanes (X > 0): from xb on, the live positions' children (kk, c), then
-                    // their grandchildren (kk, g): depth D + xlev, path bits xbits below the position
-                    const unsigned xb = nnodes + 2u;
-                    const unsigned ne1 = X >= 1u ? 2u * nb : 0u, ne2 = X >= 2u ? 4u * nb : 0u;
-                    const bool isx = SEED_X > 0 && q >= xb && q < xb + ne1 + ne2;
-                    const bool isx2 = isx && q >= xb + ne1;
-                    const unsigned xe = isx2 ? q - xb - ne1 : q - xb;
-                    const unsigned xlev = isx ? (isx2 ? 2u : 1u) : 0u;
-                    const unsigned xbits = isx ? (isx2 ? (xe & 3u) : (xe & 1u)) : 0u;
-                    const unsigned d = isnode ? div_small(q, nb, nb_rcp) : (isx ? (unsigned)D + xlev : 0u);
-                    const unsigned kk = isnode ? q - d * nb : (isx ? (isx2 ? xe >> 2 : xe >> 1) : 0u);
+                    const unsigned d = isnode ? div_small(q, nb, nb_rcp) : 0u, kk = isnode ? q - d * nb : 0u;
                     bool valid = false;
-                    const unsigned long long pp = (isnode || isx) ? position(kk, valid) : 0ull;
-                    const unsigned long long anc = !valid ? 0ull
-                                                  : isx ? ((pp << xlev) | (unsigned long long)xbits)
-                                                        : (pp >> (D - (int)d));
+                    const unsigned long long pp = isnode ? position(kk, valid) : 0ull;
+                    const unsigned long long anc = valid ? (pp >> (D - (int)d)) : 0ull;
                     unsigned li = nnodes, ri = nnodes + 1;
                     for (unsigned i = 0; i < d; ++i) {
                         const double mm = (l + r) / 2;
-                        // the node whose midpoint this step's new endpoint is: path node (i, kk), or
-                        // for a grandchild's last step its parent child (kk, c)
-                        const unsigned ia = (SEED_X == 0 || i < nlev) ? i * nb + kk : xb + 2u * kk + (xbits >> 1);
-                        if ((anc >> (d - 1 - i)) & 1ull) { l = mm; li = ia; } else { r = mm; ri = ia; }
+                        if ((anc >> (d - 1 - i)) & 1ull) { l = mm; li = i * nb + kk; } else { r = mm; ri = i * nb + kk; }
                     }
                     mid = (l + r) / 2;                                        // :187
                     if constexpr (DIAG) { asm volatile("" :: "v"(mid)); cb = clk(); }
-                    const unsigned nev = nnodes + 2u + ne1 + ne2;             // lanes that evaluate F
-                    const unsigned fq = nev <= 64 ? q : (q < nnodes ? q : 64u);
-                    if (fq < nev)
-                        fmid = integrand<FID>((isnode || isx) ? mid : (q == nnodes ? A : B), tab);   // :188
-                    if (fq < nev) fm[q] = fmid;
+                    const unsigned fq = nnodes + 2 <= 64 ? q : (q < nnodes ? q : 64u);
+                    if (fq < nnodes + 2)
+                        fmid = integrand<FID>(isnode ? mid : (q == nnodes ? A : B), tab);   // :188
+                    if (fq < nnodes + 2) fm[q] = fmid;
                     if constexpr (AQ_STAMPS && !DIAG) { asm volatile("" :: "v"(fmid)); stamp(ST_FEVAL); }
                     if (nnodes + 2 > 64 && lane < 2) fm[nnodes + lane] = integrand<FID>(lane == 0 ? A : B, tab);
                     if constexpr (DIAG) {
@@ -1160,7 +1078,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     bool refine = false;
                     double leafarea = 0.0;
-                    if (isnode || isx) {
+                    if (isnode) {
                         fl = fm[li];
                         fr = fm[ri];
                         const double lrarea = (fl + fr) * (r - l) / 2;        // :185
@@ -1185,30 +1103,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     }
                     // a surviving position node emits its children pair (depth D + 1)
                     alive = isnode && valid && (int)d == D && dstar >= nlev && D + 1 < max_depth;
-                    if constexpr (SEED_X > 0) {
-                        if (X > 0u) {
-                            // the live positions' children, then grandchildren: each exists when its
-                            // parent refines; every existing one is a task of this share (no shared
-                            // ancestors below a position); the deepest level's refining nodes are the seeds
-                            const unsigned long long am_pos = __ballot(alive);
-                            bool exists = isx && valid && ((am_pos >> (nlev * nb - nb + kk)) & 1ull);
-                            const unsigned long long am_r1 = __ballot(exists && !isx2 && refine);
-                            if (isx2) exists = exists && ((am_r1 >> (xb + 2u * kk + (xbits >> 1))) & 1ull);
-                            if (exists) {
-                                ++acc.tasks;
-                                acc.maxd = max(acc.maxd, d + 1u);
-                                if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
-                                if (!refine) {
-                                    dd_add(acc.hi, acc.lo, leafarea / area_scale<FID>());   // :199 -> :149
-                                    ++acc.leaves;
-                                    if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
-                                }
-                            }
-                            alive = exists && refine && xlev == X;
-                        }
-                    }
                     // (the per-burst cap's maxdt counts pushed pairs only: the seeds' depth goes here)
-                    if (burst_cap && alive) acc.maxd = max(acc.maxd, dt_seed + 1u);
+                    if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
                     if constexpr (DIAG) cp2 = clk();
                 } else {
                     for (unsigned q0 = 0; q0 < nnodes + 2; q0 += 64) {
@@ -1303,7 +1199,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     // a pair holds its endpoints halved (aq_device.h pair_step_halves; exact)
                     s_a[j] = 0.5 * l; s_b[j] = 0.5 * r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
                     const bool span = FID == F_COSH4 && cosh_main_span(l, r);
-                    s_dt[j] = dt_seed | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
+                    s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }
                 bot = 0;
                 top = (unsigned)__popcll(am);
@@ -1324,12 +1220,26 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
 
             if (phase == 2) break;
+            // a leader hands its workgroup's token back first (the atomic's round trip overlaps the flush)
+            unsigned r_idle = 0;
+            bool had_token = false;
+            if (lead && lane == 0) {
+                had_token = S.busy_token != 0;
+                if (had_token) {
+                    S.busy_token = 0;
+                    r_idle = g_add(&qc->idle[grp].v, 1u);
+                }
+            }
+            // a wave that ran dry flushes now, off the run's critical path: the workgroup's other waves
+            // while its last still works; the last one (the leader) once the end is stored or while it
+            // waits, below (every wave flushing after the end was seen had cost a lone launch ~1 us, r04j)
+            if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
             if (!lead) {
                 __builtin_amdgcn_s_sleep(4);
                 __builtin_amdgcn_wave_barrier();
                 continue;
             }
-            // ---- leader: this workgroup has no work; hand its token back and wait for a chunk
+            // ---- leader: this workgroup has no work; wait for a chunk or the end
             unsigned long long tl = DIAG ? rtc() : 0ull;
             stamp(ST_LEAD);
             if constexpr (DIAG) {
@@ -1340,31 +1250,23 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             int cmd = -1;   // >= 0 chunk slot, -1 exit, -2 error
             unsigned cnt = 0;
-            unsigned r_idle = 0;
-            bool had_token = false;
+            bool last = false;   // this workgroup's idle transition ended the run
             if (lane == 0) {
-                had_token = S.busy_token != 0;
-                if (had_token) {
-                    S.busy_token = 0;
-                    r_idle = g_add(&qc->idle[grp].v, 1u);
-                }
-            }
-            // (IDLE_FLUSH: the leader's own flush runs while that atomic is in flight)
-            if constexpr (IDLE_FLUSH) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
-            if (lane == 0) {
-                bool last = false;   // this workgroup's idle transition ended the run
                 if (had_token && r_idle + 1u == grp_size)   // the group's last busy workgroup
                     last = g_add((int*)&qc->tokens.v, -1) - 1 == -t0;
-                if (last) {
-                    st_wt(&qc->done.v, 1u);
-                    if constexpr (DONE_GROUPS)
-                        for (int g = 0; g < NGROUP; ++g) st_wt(&qc->done_g[g].v, 1u);
-                } else {
-                    // LAZY_TICKET: the end flag alone first (one load per spin, no ticket)
+                if (last)
+                    for (int g = 0; g < NGROUP; ++g) st_wt(&qc->done[g].v, 1u);
+            }
+            // the leader's flush: behind the end's stores (the run's last leader: the other workgroups
+            // see the end meanwhile), or before its wait
+            flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+            if (lane == 0) {
+                if (!last) {
+                    // per-CU launches: the end flag alone first (one load per spin, no ticket)
                     bool ended = false;
-                    if constexpr (PCU && LAZY_TICKET > 0) {
+                    if constexpr (PCU) {
                         for (unsigned spins = 0; spins < LAZY_TICKET; ++spins) {
-                            if (ld_wt(DONE_GROUPS ? &qc->done_g[grp].v : &qc->done.v)) { ended = true; break; }
+                            if (ld_wt(&qc->done[grp].v)) { ended = true; break; }
                             __builtin_amdgcn_s_sleep(AQ_LEAD_SLEEP);
                         }
                     }
@@ -1379,7 +1281,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     for (unsigned spins = 0; !ended; ++spins) {
                         // both words are read every spin, issued together (one latency per spin)
                         const unsigned rv = h < P.qcap ? ld_wt(&P.ready[(size_t)h * READY_STRIDE]) : 0u;
-                        const unsigned dn = ld_wt(DONE_GROUPS ? &qc->done_g[grp].v : &qc->done.v);
+                        const unsigned dn = ld_wt(&qc->done[grp].v);
                         if (rv == P.epoch) { cmd = (int)h; break; }
                         if (dn) { cmd = -1; break; }
                         if ((spins & 63u) == 63u) {
@@ -1409,9 +1311,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if constexpr (DIAG) { if (lane == 0 && cmd < 0) atomicMax(&s_dg[DG_T_DONE], rtc()); }
             if (cmd < 0) stamp(ST_DONE);
             if (cmd < 0) {
-                wave_lock(&S.lock, lane, lock_spins);
-                if (lane == 0) S.phase = 2;
-                wave_unlock(&S.lock, lane);
+                // the end (or an error): no other wave writes the phase any more (all are idle), so one
+                // store, no lock
+                if (lane == 0) __hip_atomic_store(&S.phase, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_wave_barrier();
                 break;
             }
             // load the chunk into the (empty) pool, take this workgroup's token back
@@ -1449,7 +1352,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
 
         // ---- keep the ring from overflowing: its bottom 64 pairs go to the cellar, else the pool,
         //      else an HBM chunk
-        if (size > (unsigned)HI) {
+        if (size > (unsigned)(WCAP - 64)) {
             if (pf_n) {
                 // a prefetch in flight is cancelled: its pairs never left the cellar (the loads land in
                 // registers nobody reads; the next spill writes above them)
@@ -1596,21 +1499,15 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // ds_read_b64 (12 array cycles) rather than three ds_read2st64_b64 (24). The window, the cellar lines and the accounting
         // count S = ring + held pairs; a burst starts with every pair in the ring and ends by pushing
         // the held ones back on top. Capacity: a round moves at most one pair per active lane into the
-        // ring, so the ring never holds more than S at a round's start; S <= HI = WCAP - 64 NP then
-        // leaves room for the round (S grows by <= 64 NP) and the final push.
+        // ring, so the ring never holds more than S at a round's start; S <= WCAP - 64 then leaves
+        // room for the round (S grows by <= 64) and the final push.
         unsigned b_S = b_size, b_S0 = b_size;   // ring + held; the accounting base (moves with the cellar)
-        // the held pairs, NP per lane (cdw: the dt word); b_am[p]: the lanes that hold pair p
-        unsigned long long b_am[NP];
-        double ca[NP], cb[NP], cfa[NP], cfm[NP], cfb[NP], cdw[NP];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {
-            b_am[q] = 0;
-            ca[q] = cb[q] = cfa[q] = cfm[q] = cfb[q] = cdw[q] = 0.0;
-        }
+        unsigned long long b_am = 0;
+        double ca = 0.0, cb = 0.0, cfa = 0.0, cfm = 0.0, cfb = 0.0, cdw = 0.0;   // the held pair (cdw: the dt word)
         unsigned b_lo1, b_span;
         auto window = [&]() {
             b_lo1 = (b_pf != 0u ? (unsigned)PF_BELOW : (b_ctop > 0u ? (unsigned)PF_ISSUE : 0u)) + 1u;
-            b_span = (unsigned)HI + 1u - b_lo1;
+            b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
         };
         window();
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
@@ -1622,96 +1519,64 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             unsigned long long c0 = 0, c1 = 0;
             if constexpr (DIAG) c0 = clk();
             asm volatile("s_setprio 3");
-            // ---- fill: the idle pair slots take the ring's top k pairs (rank among the idle slots: slot
-            //      0's idle lanes first, then slot 1's)
-            unsigned long long need[NP];
-            unsigned nbase[NP], ntot = 0;
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                need[q] = ~b_am[q];
-                nbase[q] = ntot;
-                ntot += (unsigned)__popcll(need[q]);
-            }
-            const unsigned k = min(ntot, b_top - b_bot);
+            // ---- fill: the idle lanes take the ring's top k pairs (rank j among the idle lanes)
+            const unsigned long long need = ~b_am;
+            const unsigned k = min((unsigned)__popcll(need), b_top - b_bot);
+            const unsigned jr = mbcnt(need);
+            const unsigned long long fmsk = __ballot(jr < k) & need;
             b_top -= k;
-            const unsigned rs = ring_slot(b_top);
-            unsigned long long am[NP];
-            unsigned na = 0;
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                const unsigned jr = nbase[q] + mbcnt(need[q]);
-                const unsigned long long fmsk = __ballot(jr < k) & need[q];
-                const unsigned paddr = ring_addr(ring8, rs + jr, ring_vmask);
-                lds_pop6_masked(fmsk, paddr, paddr + 3u * 50u * 512u, ca[q], cb[q], cfa[q], cfm[q], cfb[q], cdw[q]);
-                am[q] = b_am[q] | fmsk;
-                na += (unsigned)__popcll(am[q]);
-            }
-            unsigned long long dtw[NP];
-            unsigned dt[NP];
-            unsigned long long nospan = 0ull;   // lanes with a pair lacking SPAN_BIT (one sign test each)
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                dtw[q] = (unsigned long long)__double_as_longlong(cdw[q]);
-                dt[q] = (unsigned)dtw[q];
-                if constexpr (FID == F_COSH4) nospan |= __ballot((int)dt[q] >= 0) & am[q];
-            }
-            Step2 st[2 * NP];
-            double hm[NP];
-            pair_step_halves_n<FID, NP>(ca, cb, cfa, cfm, cfb, eps2, tab, st, hm, kk, FID == F_COSH4 ? 2 : -1, nospan);
+            const unsigned paddr = ring_addr(ring8, ring_slot(b_top) + jr, ring_vmask);
+            lds_pop6_masked(fmsk, paddr, paddr + 3u * 50u * 512u, ca, cb, cfa, cfm, cfb, cdw);
+            const unsigned long long am = b_am | fmsk;
+            const unsigned na = (unsigned)__popcll(am);
+            const double pa = ca, pb = cb, pfa = cfa, pfm = cfm, pfb = cfb;
+            const unsigned long long dtw = (unsigned long long)__double_as_longlong(cdw);
+            const unsigned dt = (unsigned)dtw;
+            Step2 st[2];
+            // the lanes whose pair lacks SPAN_BIT (both midpoints lie in the pair's interval, so one
+            // sign test of the pair word)
+            unsigned long long nospan = 0ull;
+            if constexpr (FID == F_COSH4) nospan = __ballot((int)dt >= 0);
+            double pm, hm;
+            pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
             asm volatile("s_setprio 0");
+            const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
+            unsigned long long okm = am;
+            if constexpr (!burst_cap) {
+                const unsigned long long dm = __ballot((dt & 255u) < (unsigned)(max_depth - 1));
+                okm = am & dm;
+                const unsigned long long atcap = am & ~dm;
+                if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
+            }
+            const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
             b_n += na;   // tasks 2 na; accepted: once per burst from the growth of S (below)
-            unsigned long long mask0[NP], mask1[NP];
-            unsigned long long cdtw[NP];
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                const unsigned long long r0m = __ballot(st[2 * q].refine), r1m = __ballot(st[2 * q + 1].refine);
-                unsigned long long okm = am[q];
-                if constexpr (!burst_cap) {
-                    const unsigned long long dm = __ballot((dt[q] & 255u) < (unsigned)(max_depth - 1));
-                    okm = am[q] & dm;
-                    const unsigned long long atcap = am[q] & ~dm;
-                    if (__builtin_expect(atcap != 0ull, 0)) b_dv |= atcap & (r0m | r1m);
-                }
-                const unsigned long long l0m = am[q] & ~r0m, l1m = am[q] & ~r1m;
-                mask0[q] = okm & r0m;
-                mask1[q] = okm & r1m;
-                cdtw[q] = dtw[q] + 1ull;   // depth + 1, same integral
-                const unsigned cdt = (unsigned)cdtw[q];
-                masked_acc3(acc.r, st[2 * q].area2, l0m, st[2 * q + 1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt[q],
-                            burst_cap ? (mask0[q] | mask1[q]) : am[q]);
-                if constexpr (DIAG) {
-                    const int rtag = (int)dt_tag(dt[q]);
-                    b_mixed |= (__ballot(rtag != tag) & am[q]) != 0ull;
-                }
-                if (HIST) {
-                    const unsigned d = dt[q] & 255u;
-                    if (__builtin_amdgcn_inverse_ballot_w64(am[q])) {
-                        atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
-                        const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
-                        if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
-                    }
+            const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
+            const unsigned long long cdtw = dtw + 1ull;   // depth + 1, same integral
+            const unsigned cdt = (unsigned)cdtw;
+            masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
+                        burst_cap ? (mask0 | mask1) : am);
+            if constexpr (DIAG) {
+                const int rtag = (int)dt_tag(dt);
+                b_mixed |= (__ballot(rtag != tag) & am) != 0ull;
+            }
+            if (HIST) {
+                const unsigned d = dt & 255u;
+                if (__builtin_amdgcn_inverse_ballot_w64(am)) {
+                    atomicAdd(&P.ctls[P.first_slot + tag].hist[d], 2ull);
+                    const unsigned nl = ((l0m >> lane) & 1u) + ((l1m >> lane) & 1u);
+                    if (nl) atomicAdd(&P.ctls[P.first_slot + tag].hist[AQ_MAX_LEVELS + d], (unsigned long long)nl);
                 }
             }
             if constexpr (DIAG) c1 = clk();
             // ---- task 1's children [m, b] go on the ring (:192-197); task 0's [a, m] stay in the lane
-            const unsigned ps = ring_slot(b_top);
-            unsigned pbase = 0, nkeep = 0;
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                lds_push6_masked(mask1[q], ring_addr(ring8, ps + pbase + mbcnt(mask1[q]), ring_vmask), hm[q], cb[q],
-                                 cfm[q], st[2 * q + 1].fmid, cfb[q], __longlong_as_double((long long)cdtw[q]));
-                pbase += (unsigned)__popcll(mask1[q]);
-                nkeep += (unsigned)__popcll(mask0[q]);
-            }
-            b_top += pbase;
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                cb[q] = hm[q];
-                cfb[q] = cfm[q];
-                cfm[q] = st[2 * q].fmid;
-                cdw[q] = __longlong_as_double((long long)cdtw[q]);
-                b_am[q] = mask0[q];
-            }
+            lds_push6_masked(mask1, ring_addr(ring8, ring_slot(b_top) + mbcnt(mask1), ring_vmask), hm, pb, pfm,
+                             st[1].fmid, pfb, __longlong_as_double((long long)cdtw));
+            b_top += (unsigned)__popcll(mask1);
+            cb = hm;
+            cfb = pfm;
+            cfm = st[0].fmid;
+            cdw = __longlong_as_double((long long)cdtw);
+            b_am = mask0;
             if constexpr (DIAG) {
                 if (lane == 0) {
                     const unsigned long long c2 = clk();
@@ -1724,7 +1589,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     atomicAdd(&s_dg[DG_ACTIVE_TASKS], 2ull * na);
                 }
             }
-            b_S = (b_top - b_bot) + nkeep;
+            b_S = (b_top - b_bot) + (unsigned)__popcll(mask0);
             --b_rem;
             unsigned span_r = b_rem != 0u ? b_span : 0u;
             asm("" : "+s"(span_r));
@@ -1736,14 +1601,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             asm volatile("" : "+s"(b_re));
             const unsigned sz = b_S;
             if (b_re != 0u && sz != 0u) {
-                // a cellar edge: the spill needs SPILL pairs in the ring (always with one held pair per
-                // lane: S > WCAP - 64 leaves >= WCAP - 128; with two the burst ends instead, and the
-                // final push fits: S <= HI + 64 NP = WCAP); S <= PF_BELOW leaves room for the landing
-                if (sz > (unsigned)HI) {
-                    // down to the window again (a round adds up to 64 NP pairs: with two held pairs per lane
-                    // one chunk may not do), or the burst ends and the outer loop spills the rest
-                    while (b_S > (unsigned)HI && b_ctop + (unsigned)SPILL <= (unsigned)CCAP &&
-                           b_top - b_bot >= (unsigned)SPILL) {
+                // a cellar edge: S > WCAP - 64 leaves >= WCAP - 128 >= SPILL pairs in the ring; S <=
+                // PF_BELOW leaves the ring room for the landing
+                if (sz > (unsigned)(WCAP - 64)) {
+                    if (b_ctop + (unsigned)SPILL <= (unsigned)CCAP) {
                         if (b_pf) {
                             b_ctop += b_pf;
                             b_pf = 0;
@@ -1753,8 +1614,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                         b_bot += (unsigned)SPILL;
                         b_S -= (unsigned)SPILL;
                         b_S0 -= (unsigned)SPILL;
+                        b_go = true;
                     }
-                    b_go = b_S <= (unsigned)HI;
                 } else if (b_pf) {
                     if (b_bot < 64u) {
                         b_bot += (unsigned)WCAP;
@@ -1779,12 +1640,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if (!b_go) break;
         }
         // the held pairs back on top of the ring
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {
-            lds_push6_masked(b_am[q], ring_addr(ring8, ring_slot(b_top) + mbcnt(b_am[q]), ring_vmask), ca[q], cb[q], cfa[q],
-                             cfm[q], cfb[q], cdw[q]);
-            b_top += (unsigned)__popcll(b_am[q]);
-        }
+        lds_push6_masked(b_am, ring_addr(ring8, ring_slot(b_top) + mbcnt(b_am), ring_vmask), ca, cb, cfa, cfm, cfb,
+                         cdw);
+        b_top += (unsigned)__popcll(b_am);
         bot = b_bot;
         ctop = b_ctop;
         pf_n = b_pf;
