@@ -127,6 +127,32 @@ __global__ __launch_bounds__(256) void k_copy4(const d2* __restrict__ in, size_t
     }
 }
 
+// The HBM baseline shapes: OUTS (1 or 2) 16-B stores per 16-B load, U loads in flight per thread
+// before their stores, non-temporal (NT) or default cache policy; a grid-stride loop over n16 pieces.
+template <int OUTS, int U, bool NT>
+__global__ __launch_bounds__(256) void k_copy_u(const d2* __restrict__ in, size_t n16, d2* __restrict__ out) {
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t i0 = (size_t)blockIdx.x * 256 * U + threadIdx.x; i0 < n16; i0 += stride) {
+        d2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = i0 + (size_t)u * 256;
+            if (i < n16) v[u] = NT ? __builtin_nontemporal_load(in + i) : in[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = i0 + (size_t)u * 256;
+            if (i < n16) {
+#pragma unroll
+                for (int o = 0; o < OUTS; ++o) {
+                    if (NT) __builtin_nontemporal_store(v[u], out + (size_t)o * n16 + i);
+                    else out[(size_t)o * n16 + i] = v[u];
+                }
+            }
+        }
+    }
+}
+
 // write-only and read-only passes of the same sizes
 __global__ __launch_bounds__(256) void k_write(Rec* __restrict__ out, unsigned n_out) {
     const unsigned i = blockIdx.x * 256 + threadIdx.x;
@@ -219,6 +245,39 @@ int main() {
         const double bytes = 3.0 * 16.0 * (double)n16;
         printf("{\"variant\": \"copy16_nt_x%zu\", \"bytes\": %.0f, \"us_median\": %.2f, \"us_min\": %.2f, \"GBps_median\": %.1f}\n",
                mult, bytes, t[6], t[0], bytes / (t[6] * 1e-6) / 1e9);
+        CHECK(hipFree(ci));
+        CHECK(hipFree(co));
+    }
+    // the baseline shapes at 10x the level's input (1.06 GB read): 1:1 and 1:2, unroll 1 / 4, both policies
+    {
+        const size_t n16 = (size_t)n * 2 * 10;
+        d2 *ci, *co;
+        CHECK(hipMalloc(&ci, n16 * 16));
+        CHECK(hipMalloc(&co, 2 * n16 * 16));
+        CHECK(hipMemset(ci, 0, n16 * 16));
+        CHECK(hipMemset(co, 0, 2 * n16 * 16));
+        auto shape = [&](const char* name, int outs, auto launch) -> int {
+            std::vector<float> t;
+            for (int rep = 0; rep < 12; ++rep) {
+                CHECK(hipEventRecord(a));
+                launch();
+                CHECK(hipEventRecord(b));
+                CHECK(hipEventSynchronize(b));
+                float ms; CHECK(hipEventElapsedTime(&ms, a, b)); t.push_back(ms * 1e3f);
+            }
+            std::sort(t.begin(), t.end());
+            const double bytes = (1.0 + outs) * 16.0 * (double)n16;
+            printf("{\"variant\": \"%s\", \"bytes\": %.0f, \"us_median\": %.2f, \"us_min\": %.2f, \"GBps_median\": %.1f}\n",
+                   name, bytes, t[6], t[0], bytes / (t[6] * 1e-6) / 1e9);
+            return 0;
+        };
+        const int g = 2048;
+        if (shape("copy1to1_u1", 1, [&] { hipLaunchKernelGGL((k_copy_u<1, 1, false>), dim3(g), dim3(256), 0, 0, ci, n16, co); })) return 1;
+        if (shape("copy1to1_u4", 1, [&] { hipLaunchKernelGGL((k_copy_u<1, 4, false>), dim3(g), dim3(256), 0, 0, ci, n16, co); })) return 1;
+        if (shape("copy1to1_u4_nt", 1, [&] { hipLaunchKernelGGL((k_copy_u<1, 4, true>), dim3(g), dim3(256), 0, 0, ci, n16, co); })) return 1;
+        if (shape("copy1to2_u1", 2, [&] { hipLaunchKernelGGL((k_copy_u<2, 1, false>), dim3(g), dim3(256), 0, 0, ci, n16, co); })) return 1;
+        if (shape("copy1to2_u4", 2, [&] { hipLaunchKernelGGL((k_copy_u<2, 4, false>), dim3(g), dim3(256), 0, 0, ci, n16, co); })) return 1;
+        if (shape("copy1to2_u4_nt", 2, [&] { hipLaunchKernelGGL((k_copy_u<2, 4, true>), dim3(g), dim3(256), 0, 0, ci, n16, co); })) return 1;
         CHECK(hipFree(ci));
         CHECK(hipFree(co));
     }
