@@ -145,6 +145,11 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 // spins, before it takes a queue ticket -- at a lone launch's end 255 leaders drawing tickets from one
 // counter (~12 ns each, MI355X_MICROARCH.md "fanin") held the last of them ~3 us past the end (r04j/k)
 constexpr unsigned LAZY_TICKET = 64;
+// Per-CU launches of the skewed integrand (sin(1/x): one region holds nearly all of the tree): a burst
+// that starts with at least HEAVY_S pairs runs its rounds at priority 3 throughout; the others start
+// at 1 and drop to 0 after their F chains -- the waves holding the most work win the SIMD's issue
+// (config-4 lone 80.6 -> 76.8 us; for cosh4 no gain at thresholds 32 / 64 / 128, r04p)
+constexpr unsigned HEAVY_S = 64;
 enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
              ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_N, ST_STRIDE = 16 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
@@ -1510,6 +1515,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             b_span = (unsigned)(WCAP - 64) + 1u - b_lo1;
         };
         window();
+        constexpr bool prio_by_load = PCU && FID == F_SIN_RECIP;
+        const bool b_heavy = prio_by_load && b_S >= HEAVY_S;
         const unsigned b_max = give_rounds - b_poll % give_rounds;   // rounds up to the give / poll round
         unsigned b_rem = b_max;
         __builtin_amdgcn_s_waitcnt(0xC07F);   // (see below: no wait in front of every round's pop)
@@ -1518,7 +1525,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         for (;;) {
             unsigned long long c0 = 0, c1 = 0;
             if constexpr (DIAG) c0 = clk();
-            asm volatile("s_setprio 3");
+            if (!prio_by_load || b_heavy) asm volatile("s_setprio 3");
+            else asm volatile("s_setprio 1");
             // ---- fill: the idle lanes take the ring's top k pairs (rank j among the idle lanes)
             const unsigned long long need = ~b_am;
             const unsigned k = min((unsigned)__popcll(need), b_top - b_bot);
@@ -1539,7 +1547,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if constexpr (FID == F_COSH4) nospan = __ballot((int)dt >= 0);
             double pm, hm;
             pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
-            asm volatile("s_setprio 0");
+            if (!prio_by_load || !b_heavy) asm volatile("s_setprio 0");
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
             unsigned long long okm = am;
             if constexpr (!burst_cap) {
