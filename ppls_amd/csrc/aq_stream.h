@@ -82,11 +82,11 @@ constexpr int JOB_RUN_MAX = AQ_JOB_RUN_MAX;   // most jobs one claim takes (whol
 __host__ __device__ constexpr int seed_depth(unsigned long long V) {
     return V <= 1ull ? AQ_S_W1 : 63 - __builtin_clzll(V) + S_W;
 }
-// positions per share, ceil(2^D / V), for D = seed_depth(V) -- in (2^(S_W-1), 2^S_W] when V > 1, so a
-// count-down of at most 2^(S_W-1) steps instead of a 64-bit division (cold code at every seeding)
+// positions per share, ceil(2^D / V): with L = floor(log2 V), 2^D / V lies in (2^(D-L-1), 2^(D-L)], so a
+// count-down of at most 2^(D-L-1) steps instead of a 64-bit division (cold code at every seeding)
 __host__ __device__ constexpr unsigned seed_nb(int D, unsigned long long V) {
     if (V <= 1ull) return 1u << D;
-    unsigned nb = 1u << S_W;
+    unsigned nb = 1u << (D - (63 - __builtin_clzll(V)));
     while (nb > 1u && (unsigned long long)(nb - 1u) * V >= (1ull << D)) --nb;
     return nb;
 }
@@ -1044,8 +1044,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     return j;
                 };
                 unsigned long long cp1 = 0, cp2 = 0;
-                bool alive = false;
+                bool alive = false, alive2 = false;   // alive2: the dual path's second node per lane
                 double l = A, r = B, fl = 0.0, fr = 0.0, mid = 0.0, fmid = 0.0;
+                double l2 = A, r2 = B, fl2 = 0.0, fr2 = 0.0, fmid2 = 0.0;
                 if (nnodes <= 64) {
                     // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
                     // decision; the first leaf depth of every position comes from ONE ballot
@@ -1111,6 +1112,96 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     // (the per-burst cap's maxdt counts pushed pairs only: the seeds' depth goes here)
                     if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
                     if constexpr (DIAG) cp2 = clk();
+                } else if (FID == F_SIN_RECIP && nnodes + 2u <= 128u) {
+                    // dual path (the skewed integrand's lone launches, seeded one level deeper: aq_abi.inc):
+                    // lane q owns nodes q and q + 64 -- the fast path twice over, the two F chains
+                    // interleaved, the first leaf depth from two ballots over a 128-bit column mask
+                    unsigned long long c0lo = 0, c0hi = 0;   // column 0's nodes (uniform)
+                    for (unsigned d = 0; d < nlev; ++d) {
+                        const unsigned b = d * nb;
+                        if (b < 64u) c0lo |= 1ull << b; else c0hi |= 1ull << (b - 64u);
+                    }
+                    c0lo = uni(c0lo);
+                    c0hi = uni(c0hi);
+                    bool isn[2], vld[2], rfn[2];
+                    unsigned dd[2], kc[2], lix[2], rix[2];
+                    unsigned long long ppx[2];
+                    double lx[2], rx[2], mx[2], fx[2], flx[2], frx[2], lax[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const unsigned q = lane + 64u * (unsigned)h;
+                        isn[h] = q < nnodes;
+                        dd[h] = isn[h] ? div_small(q, nb, nb_rcp) : 0u;
+                        kc[h] = isn[h] ? q - dd[h] * nb : 0u;
+                        vld[h] = false;
+                        ppx[h] = isn[h] ? position(kc[h], vld[h]) : 0ull;
+                        const unsigned long long anc = vld[h] ? (ppx[h] >> (D - (int)dd[h])) : 0ull;
+                        double ll = A, rr = B;
+                        unsigned li = nnodes, ri = nnodes + 1;
+                        for (unsigned i = 0; i < dd[h]; ++i) {
+                            const double mm = (ll + rr) / 2;
+                            if ((anc >> (dd[h] - 1 - i)) & 1ull) { ll = mm; li = i * nb + kc[h]; } else { rr = mm; ri = i * nb + kc[h]; }
+                        }
+                        lx[h] = ll; rx[h] = rr; lix[h] = li; rix[h] = ri;
+                        mx[h] = (ll + rr) / 2;                                    // :187
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const unsigned q = lane + 64u * (unsigned)h;
+                        fx[h] = 0.0;
+                        if (q < nnodes + 2u) fx[h] = integrand<FID>(isn[h] ? mx[h] : (q == nnodes ? A : B), tab);   // :188
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const unsigned q = lane + 64u * (unsigned)h;
+                        if (q < nnodes + 2u) fm[q] = fx[h];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        rfn[h] = false;
+                        lax[h] = 0.0;
+                        flx[h] = frx[h] = 0.0;
+                        if (isn[h]) {
+                            flx[h] = fm[lix[h]];
+                            frx[h] = fm[rix[h]];
+                            const double lrarea = (flx[h] + frx[h]) * (rx[h] - lx[h]) / 2;   // :185
+                            const double larea = (flx[h] + fx[h]) * (mx[h] - lx[h]) / 2;     // :189
+                            const double rarea = (fx[h] + frx[h]) * (rx[h] - mx[h]) / 2;     // :190
+                            rfn[h] = fabs((larea + rarea) - lrarea) > eps;                   // :191
+                            lax[h] = larea + rarea;                                          // :199
+                        }
+                    }
+                    const unsigned long long lm_lo = __ballot(isn[0] && vld[0] && !rfn[0]);
+                    const unsigned long long lm_hi = __ballot(isn[1] && vld[1] && !rfn[1]);
+                    bool alv[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const unsigned k = kc[h];   // < nb <= 64: the column's 128-bit mask is col0 << k
+                        const unsigned long long cl = c0lo << k;
+                        const unsigned long long ch = k ? ((c0hi << k) | (c0lo >> (64u - k))) : c0hi;
+                        const unsigned long long ml = lm_lo & cl, mh = lm_hi & ch;
+                        const unsigned qf = ml ? (unsigned)__builtin_ctzll(ml) : (mh ? 64u + (unsigned)__builtin_ctzll(mh) : ~0u);
+                        const unsigned dstar = qf == ~0u ? nlev : div_small(qf, nb, nb_rcp);
+                        const unsigned d = dd[h];
+                        if (isn[h] && vld[h] && d <= dstar && (ppx[h] & ((1ull << (D - (int)d)) - 1ull)) == 0ull) {
+                            ++acc.tasks;                                          // owner of node (d, k)
+                            acc.maxd = max(acc.maxd, d + 1u);
+                            if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
+                            if (d == dstar) {
+                                dd_add(acc.hi, acc.lo, lax[h] / area_scale<FID>());   // :199 -> :149
+                                ++acc.leaves;
+                                if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
+                            } else if ((int)d + 1 >= max_depth) {
+                                err |= ERRB_DEPTH;
+                            }
+                        }
+                        alv[h] = isn[h] && vld[h] && (int)d == D && dstar >= nlev && D + 1 < max_depth;
+                        if (burst_cap && alv[h]) acc.maxd = max(acc.maxd, (unsigned)D + 2u);
+                    }
+                    alive = alv[0]; l = lx[0]; r = rx[0]; fl = flx[0]; fr = frx[0]; fmid = fx[0];
+                    alive2 = alv[1]; l2 = lx[1]; r2 = rx[1]; fl2 = flx[1]; fr2 = frx[1]; fmid2 = fx[1];
+                    if constexpr (DIAG) { cp1 = clk(); cp2 = cp1; }
                 } else {
                     for (unsigned q0 = 0; q0 < nnodes + 2; q0 += 64) {
                         const unsigned q = q0 + lane;
@@ -1198,16 +1289,26 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 }
                 __builtin_amdgcn_wave_barrier();   // every read of the scratch precedes the seed writes
                 const unsigned long long am = __ballot(alive);
+                constexpr double fs = f_scale<FID>();   // the rounds' F values (exact scaling)
                 if (alive) {
                     const unsigned j = base + mbcnt(am);
-                    constexpr double fs = f_scale<FID>();   // the rounds' F values (exact scaling)
                     // a pair holds its endpoints halved (aq_device.h pair_step_halves; exact)
                     s_a[j] = 0.5 * l; s_b[j] = 0.5 * r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
                     const bool span = FID == F_COSH4 && cosh_main_span(l, r);
                     s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }
+                unsigned n_seeds = (unsigned)__popcll(am);
+                if constexpr (FID == F_SIN_RECIP) {   // the dual path's second nodes
+                    const unsigned long long am2 = __ballot(alive2);
+                    if (alive2) {
+                        const unsigned j = base + n_seeds + mbcnt(am2);
+                        s_a[j] = 0.5 * l2; s_b[j] = 0.5 * r2; s_fa[j] = fs * fl2; s_fm[j] = fs * fmid2; s_fb[j] = fs * fr2;
+                        s_dt[j] = (unsigned)(D + 1) | ((unsigned)p << TAG_SHIFT);
+                    }
+                    n_seeds += (unsigned)__popcll(am2);
+                }
                 bot = 0;
-                top = (unsigned)__popcll(am);
+                top = n_seeds;
                 stamp(ST_SEEDED);
                 if constexpr (DIAG) {
                     if (lane == 0) {
