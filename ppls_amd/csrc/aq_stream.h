@@ -4,7 +4,7 @@
 // body (:183-202) become one persistent launch:
 //   * the unit of work is a SIBLING PAIR {a, b, F(a), F(m), F(b), dt} = the two tasks [a,m] and [m,b]
 //     a refining parent pushes (:192-197); m = (a+b)/2 is recomputed from the parent's own operands
-//     (:187), so it is not stored; dt = depth | SPAN_BIT | integral << 16. A pair is six 8-byte LDS
+//     (:187), so it is not stored; dt = depth | integral << 8 | SPAN_BIT (bit 31). A pair is six 8-byte LDS
 //     fields for two tasks, and it hands every lane two independent evaluations: the K=2 cosh chains
 //     interleave (aq_libm.h cosh_main_k).
 //   * worker = WAVEFRONT. Each of the NW waves of a workgroup owns an LDS ring of pairs, and each of its
@@ -27,8 +27,8 @@
 //     tail of one integral overlaps the start of the next; launches of few take a static stride.
 //   * accepted areas / task counts accumulate per lane in registers per integral and are flushed
 //     (DPP wave reduction + device atomics into the integral's slot: counts, and the area into an
-//     exact fixed-point accumulator, aq_xsum.h) when a wave switches integral or exits (the
-//     farmer's `result += buff[0]`, :149).
+//     exact fixed-point accumulator, aq_xsum.h) when a wave switches integral, runs dry or exits
+//     (the farmer's `result += buff[0]`, :149).
 // Every decision is the reference's own arithmetic on the same operands, so the interval tree --
 // tasks and accepted counts -- is bit-identical whatever the schedule.
 #pragma once
@@ -252,9 +252,9 @@ struct alignas(128) Line {
 // count and adds (1 if the group was all-idle) - (c + 1) to T in one atomic. Every outstanding chunk
 // holds at least one token, so T stays positive while any chunk or busy workgroup exists: between a
 // group's 0 -> 1 busy transition and its T update, the taken chunk's own tokens are still counted.
-// The atomic that brings T to 0 is unique; its workgroup sets `done`, which the waiting leaders
-// poll. (One counter for all 256 workgroups made the final 256 idle transitions a ~3 us fan-in on
-// one line, then a poll of that same line by all of them.)
+// The atomic that brings T to 0 is unique; its workgroup stores the end into one `done` line per
+// group, which that group's waiting leaders poll. (One counter for all 256 workgroups made the final
+// 256 idle transitions a ~3 us fan-in on one line, then a poll of that same line by all of them.)
 constexpr int NGROUP = 8;
 struct QCtl {
     Line tail;                 // chunk slots claimed by producers
@@ -749,7 +749,6 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     asm volatile("" : "+v"(ring_vmask));   // kept in a VGPR (see ring_addr)
 
     Acc acc{0.0, 0.0, 0u, 0u, 0u, 0u, 0u, 0u};
-    // (every ring slot holds a harmless pair from the start -- the prologue: rounds read all 64 lanes' slots)
     int tag = 0;                  // integral the accumulators belong to (wave-uniform)
     unsigned ctop = 0;            // pairs in this wave's cellar (wave-uniform)
     Cellar* __restrict__ cel = P.cellar + w_all;
