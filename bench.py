@@ -15,14 +15,16 @@ ONE all-reduce inside the timed region. Launches are pipelined
 (no host sync between them); every integral's counts are verified bit-exactly and its area to
 1e-12 relative against the golden tree after timing.
 
-After the headline's timed region, two secondary passes are timed the same way (barrier + sync on
+After the headline's timed region, three secondary passes are timed the same way (barrier + sync on
 both sides, max over ranks) and reported under "secondary":
   * C3 (BASELINE configs[2]): 1 000 000 splitmix64-bounded integrals at EPSILON=1e-10, split into
     contiguous whole-integral blocks per rank, through the batch front end (aq_integrate_batch);
     verified by T = 2L - 1 for every integral, the committed per-integral prefix and the exact KAT
     (Σ leaves of the first 10 000 draws, tests/golden/batch.json);
   * C5 (BASELINE configs[4]): EPSILON=1e-12, 4096 copies of the integral per pass, each sharded over
-    the N GPUs; verified against the golden tree (counts exact, area to 1e-12).
+    the N GPUs; verified against the golden tree (counts exact, area to 1e-12);
+  * C3 again at EPSILON=1e-3 (SURVEY §8d's launch/compaction-bound run: ~1 400 tasks per integral),
+    verified the same way (the first 256 integrals, the 10 000-draw KAT: mean leaves 711.4936).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--eps E] [--no-cpu-baseline]
 
@@ -465,6 +467,7 @@ def main(argv=None):
         secondary = [
             c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist),
             c5_pass(ctx, rank, world, barrier, launch, reduce_list, dist, torch, all_reduce),
+            c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist, eps=1e-3),
         ]
         ok = ok and all(s["verified"] for s in secondary)
 
@@ -480,12 +483,23 @@ def main(argv=None):
         sys.exit(3)
 
 
-def c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist):
-    """BASELINE configs[2]: 1 M splitmix64-bounded integrals at EPSILON=1e-10, contiguous whole-integral
-    blocks per rank through aq_integrate_batch (up to 262144 integrals per persistent launch)."""
+# tests/golden/batch.json keys per C3 tolerance: per-integral leaves and areas of a prefix, and the
+# exact Σ of the KAT prefix (mean leaves 711.5 at 1e-3, 153 330.8 at 1e-10)
+C3_GOLDEN = {
+    1e-10: {"leaves": "leaves_eps1e-10", "area_hex": "area_eps1e-10_hex", "kat_n": "kat_n_eps1e-10",
+            "kat_leaves": "kat_sum_leaves_eps1e-10", "kat_tasks": "kat_sum_tasks_eps1e-10"},
+    1e-3: {"leaves": "leaves_eps1e-3_first256", "area_hex": "area_eps1e-3_first256_hex", "kat_n": "n_eps1e-3",
+           "kat_leaves": "sum_leaves_eps1e-3", "kat_tasks": "sum_tasks_eps1e-3"},
+}
+
+
+def c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist, eps=1e-10):
+    """BASELINE configs[2]: 1 M splitmix64-bounded integrals at EPSILON=1e-10 (the throughput run) or
+    1e-3 (tiny trees: launch- and seeding-bound), contiguous whole-integral blocks per rank through
+    aq_integrate_batch (up to 262144 integrals per persistent launch)."""
     import numpy as np
     import torch
-    eps = 1e-10
+    keys = C3_GOLDEN[eps]
     n = args.c3_n
     a, b = splitmix64_bounds(n)
     lo, hi = rank * n // world, (rank + 1) * n // world
@@ -505,25 +519,25 @@ def c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist):
     golden = load_json(os.path.join("tests", "golden", "batch.json")) or {}
     checked = []
     if lo == 0:
-        pre = golden.get("leaves_eps1e-10") or []
+        pre = golden.get(keys["leaves"]) or []
         m = min(len(pre), hi)
         if m:
             ok = ok and bool((acc[:m] == np.asarray(pre[:m], np.uint64)).all())
-            want = np.array([float.fromhex(v) for v in golden["area_eps1e-10_hex"][:m]])
+            want = np.array([float.fromhex(v) for v in golden[keys["area_hex"]][:m]])
             ok = ok and bool(np.all(np.abs(area[:m] - want) <= AREA_RTOL * np.abs(want)))
             checked.append(f"counts and areas of integrals 0..{m - 1} vs tests/golden/batch.json")
-        kn = golden.get("kat_n_eps1e-10", 0)
+        kn = golden.get(keys["kat_n"], 0)
         if kn and hi >= kn:
-            ok = ok and int(acc[:kn].sum()) == golden["kat_sum_leaves_eps1e-10"] \
-                and int(tasks[:kn].sum()) == golden["kat_sum_tasks_eps1e-10"]
+            ok = ok and int(acc[:kn].sum()) == golden[keys["kat_leaves"]] \
+                and int(tasks[:kn].sum()) == golden[keys["kat_tasks"]]
             checked.append(f"exact Σ leaves / tasks of the first {kn} draws (mean leaves "
-                           f"{golden['kat_sum_leaves_eps1e-10'] / kn:.4f})")
+                           f"{golden[keys['kat_leaves']] / kn:.4f})")
     # every rank's accepted / tasks / kernel seconds / verdict summed, the wall time's max
     leaves, tsum, ksum, okall = reduce_list([float(acc.sum()), float(tasks.sum()), kern_ms / 1e3, 1.0 if ok else 0.0],
                                             dist.ReduceOp.SUM)
     elapsed, = reduce_list([t1 - t0], dist.ReduceOp.MAX)
-    return {"workload": "C3 (BASELINE configs[2]): %d splitmix64-bounded cosh4 integrals at EPSILON=1e-10, "
-                        "whole integrals in contiguous blocks per rank" % n,
+    return {"workload": "C3 (BASELINE configs[2]): %d splitmix64-bounded cosh4 integrals at EPSILON=%g, "
+                        "whole integrals in contiguous blocks per rank" % (n, eps),
             "value": leaves / elapsed, "unit": "accepted subintervals/s", "ms": elapsed * 1e3,
             "integrals_per_s": n / elapsed, "accepted": int(leaves), "tasks": int(tsum),
             "frac": FLOP_PER_TASK * tsum / ksum / FP64_PEAK if ksum > 0 else None,

@@ -136,6 +136,13 @@ def test_c3_bounds_and_kat_fixture():
     n = g["kat_n_eps1e-10"]
     assert n == 10000 and g["kat_sum_tasks_eps1e-10"] == 2 * g["kat_sum_leaves_eps1e-10"] - n
     assert round(g["kat_sum_leaves_eps1e-10"] / n, 1) == 153330.8
+    # every key the bench's C3 passes read exists, for both tolerances; the eps=1e-3 KAT is SURVEY's 711.5
+    for keys in bench.C3_GOLDEN.values():
+        assert all(k in g for k in keys.values())
+    k3 = bench.C3_GOLDEN[1e-3]
+    assert g[k3["kat_tasks"]] == 2 * g[k3["kat_leaves"]] - g[k3["kat_n"]]
+    assert round(g[k3["kat_leaves"]] / g[k3["kat_n"]], 1) == 711.5
+    assert len(g[k3["leaves"]]) == len(g[k3["area_hex"]]) == 256
 
 
 def test_area_check():
