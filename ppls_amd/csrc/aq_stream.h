@@ -879,12 +879,16 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             int phase = 0;
             // a wave's first job needs no look at the pool (empty until some wave has run rounds):
             // 12 waves would otherwise queue on the lock before their first F evaluation
+            // (job_pending: the claim was read into `job` above)
             bool counted_now = false;   // counted idle just now, without the lock, and not the last
-            if (fresh && job < total_jobs) {
+            const bool pool_empty = uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                                    uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (job < total_jobs && (fresh || pool_empty)) {
+                // the next job while the pool looks empty: seeded without the lock (pool pairs that
+                // arrive meanwhile are taken at this wave's next dry spell). A wave of a tiny-tree batch
+                // (C3 at eps=1e-3: a job every ~18 us) had taken the lock before every job
                 seed = true;
-            } else if (!counted_idle && !job_pending && job >= total_jobs &&
-                       uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
-                           uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+            } else if (!counted_idle && !job_pending && job >= total_jobs && pool_empty) {
                 // nothing to seed, pool empty: count idle with one LDS atomic. Only the wave that makes
                 // the count whole takes the lock (the lead check below, pool re-read under it); the
                 // others go straight to the lock-free idle poll -- a workgroup's 12 waves running dry
@@ -976,7 +980,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 // (per-CU launches: jobs < PCU_MAXK x W, so the float estimate with its correction
                 // stands in for the integer divisions -- cold code at every lone launch)
                 const float sh_rcp = PCU ? __builtin_amdgcn_rcpf((float)shares) : 0.0f;
-                const unsigned pj = PCU ? div_small(jj, shares, sh_rcp) : jj / shares;
+                const unsigned pj = PCU ? div_small(jj, shares, sh_rcp) : (shares == 1u ? jj : jj / shares);
                 const int p = (int)((in_tail ? tail_from : 0u) + pj);
                 const unsigned shard_p = P.shard_of ? (unsigned)uni(P.shard_of[p]) : (unsigned)P.shard;
                 unsigned sh = jj - pj * shares;

@@ -25,6 +25,8 @@ for step in "$@"; do
     bench12) run bench12 400 python bench.py --eps 1e-12 --batch 4096 --steps 4 --warmup 1 --no-cpu-baseline ;;
     lone)    run lone 120 python tools/try_single.py ;;
     wall)    run wall 120 python tools/try_wall.py ;;
+    tiny)    run tiny 120 python tools/try_tiny.py ;;
+    tinyvar) for so in ppls_amd/_build/${AB_GLOB_T:-libaquad_*.so}; do n=$(basename $so .so); AQ_LIB=$PWD/$so run tiny_$n 120 python tools/try_tiny.py; done ;;
     lonecoop) AQ_COOP=1 run lone_coop 120 python tools/try_single.py ;;
     shared2) BENCH_SHARED_GPU=1 run shared2 400 python bench.py --gpus 2 --steps 4 --warmup 1 --c3-n 131072 ;;
     diag)    run diag_1e10 120 python tools/diag_single.py --eps 1e-10 && run diag_1task 120 python tools/diag_single.py --eps 1e30 ;;
