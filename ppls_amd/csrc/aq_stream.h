@@ -214,10 +214,10 @@ static_assert(PF_ISSUE >= PF_BELOW && PF_BELOW + 64 <= WCAP - 64, "a landed pref
 // and the burst goes on, where round 2 left the burst for the outer loop (~60 VALU and ~70 SALU of
 // re-checks and state moves per exit, 0.24 exits per round: tools/ring_sim.py, PMC r03e).
 //
-// Wave priority (r03, profiles/r03s-r03u): each round runs at s_setprio 3 from its pop to the end of
-// its two F chains and at 0 for its tail (ballots, exec windows, pushes, loop control) and everything
-// outside the rounds. The three waves of a SIMD are usually in different phases; the priority lets
-// the one in its latency-bound chain issue ahead of a sibling's SALU-heavy tail.
+// Wave priority. r03's popped round ran at s_setprio 3 from its pop to the end of its two F chains and
+// at 0 for its tail (-0.6..-0.8 %, profiles/r03s-r03u); the carried round is faster WITHOUT it
+// (-0.9 %, three A/B rounds, profiles/r04z/ab.txt), so only the sin(1/x) per-CU instance still sets
+// priorities (its heaviest waves, below).
 //
 // Depth cap checked once per burst (r03): a round pushes every refining task's children and keeps, per
 // lane, the deepest REFINING pair it saw (masked max, as before over the popped pairs); the burst's
@@ -1629,8 +1629,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         for (;;) {
             unsigned long long c0 = 0, c1 = 0;
             if constexpr (DIAG) c0 = clk();
-            if (!prio_by_load || b_heavy) asm volatile("s_setprio 3");
-            else asm volatile("s_setprio 1");
+            if constexpr (prio_by_load) {
+                if (b_heavy) asm volatile("s_setprio 3");
+                else asm volatile("s_setprio 1");
+            }
             // ---- fill: the idle lanes take the ring's top k pairs (rank j among the idle lanes)
             const unsigned long long need = ~b_am;
             const unsigned k = min((unsigned)__popcll(need), b_top - b_bot);
@@ -1651,7 +1653,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             if constexpr (FID == F_COSH4) nospan = __ballot((int)dt >= 0);
             double pm, hm;
             pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
-            if (!prio_by_load || !b_heavy) asm volatile("s_setprio 0");
+            if constexpr (prio_by_load) { if (!b_heavy) asm volatile("s_setprio 0"); }
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
             unsigned long long okm = am;
             if constexpr (!burst_cap) {
