@@ -105,15 +105,18 @@ constexpr int GIVE_MIN = AQ_GIVE_MIN;        // a busy wave feeds the pool for i
 constexpr int DONATE_MIN = 64;      // pool pairs needed before a workgroup donates from its pool
 #ifndef AQ_POLL_ROUNDS
 // A/B r01q (8192 integrals, eps 1e-10): 16 34.26, 32 33.35, 64 32.95 ms per launch; r03 (in-burst
-// moves, wave priority; the bench's 32768-integral launch, profiles/r03x): 128 with GIVE 64
-#define AQ_POLL_ROUNDS 128
+// moves, wave priority; the bench's 32768-integral launch, profiles/r03x): 128 with GIVE 64; r04: 256
+// with GIVE 128 (below; 128 is the largest give period the depth byte allows at AQ_MAX_LEVELS 128)
+#define AQ_POLL_ROUNDS 256
 #endif
 constexpr int POLL_ROUNDS = AQ_POLL_ROUNDS;     // a busy wave refreshes its view of the HBM queue every POLL_ROUNDS rounds
 #ifndef AQ_GIVE_ROUNDS
 // r02 (burst loop, PF_BELOW 64): 8 -> 16 -> 32 rounds 28.15 -> 27.93 ms... 64 slower; C3 unchanged.
 // r03 (bursts no longer end at cellar moves, so the give / poll round is their main end): 64 / 128 with
-// 60 k-task jobs -1.8 % on the bench launch (profiles/r03x), 16 +1.5 %, 128 / 256 -0.5 %
-#define AQ_GIVE_ROUNDS 64
+// 60 k-task jobs -1.8 % on the bench launch (profiles/r03x), 16 +1.5 %, 128 / 256 -0.5 %; r04 (carried
+// pairs: a burst's end pushes the held pairs back, so longer bursts pay): 128 / 256 -0.8 % against
+// 64 / 128 on the bench's 32768-integral launch (profiles/r04k2/ab.txt)
+#define AQ_GIVE_ROUNDS 128
 #endif
 constexpr int GIVE_ROUNDS = AQ_GIVE_ROUNDS;      // ... and looks for idle siblings every GIVE_ROUNDS rounds
 #ifndef AQ_SKEWED_GIVE
