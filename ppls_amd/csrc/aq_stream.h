@@ -90,6 +90,15 @@ __host__ __device__ constexpr unsigned seed_nb(int D, unsigned long long V) {
     while (nb > 1u && (unsigned long long)(nb - 1u) * V >= (1ull << D)) --nb;
     return nb;
 }
+// a job's seed depth: seed_depth(V), one level deeper where the seeding's one-wave fast path
+// ((D + 1) levels x nb positions <= 64 nodes) still holds the deeper seeding -- the bench's adaptive
+// jobs (V ~ 24: 3 -> 6 positions per share) and whole-integral jobs (V = 1: 4 -> 8 positions); not a
+// lone launch (V = 3072: 42 -> 90 nodes). r04n A/B at 32768 integrals: -0.8 %, C3 unchanged
+// (profiles/r04n2). The oracle's shard partition restates this rule (tests' device_seed_S).
+__host__ __device__ constexpr int seed_depth_job(unsigned long long V) {
+    return (unsigned long long)(seed_depth(V) + 2) * seed_nb(seed_depth(V) + 1, V) <= 64ull
+        ? seed_depth(V) + 1 : seed_depth(V);
+}
 // q / nb for small q (seeding's lane -> node map): the float estimate q * rcp(nb), then one
 // correction each way (exact whenever the estimate is off by at most one)
 __device__ __forceinline__ unsigned div_small(unsigned q, unsigned nb, float rnb) {
@@ -187,8 +196,10 @@ constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's 
 #endif
 #ifndef AQ_TASKS_PER_JOB
 // A/B at 8192 integrals per launch (r01): 8k 35.4, 15k 33.7, 25k 33.6, 40k 33.1, 60k 33.3, 100k 37.0 ms;
-// r03 at the bench's 32768 per launch (profiles/r03x): 60 k -1.8 % with give / poll 64 / 128, 80 k -1.3 %
-#define AQ_TASKS_PER_JOB 60000
+// r03 at the bench's 32768 per launch (profiles/r03x): 60 k -1.8 % with give / poll 64 / 128, 80 k -1.3 %;
+// r04n (give / poll 128 / 256, one level deeper seeding, profiles/r04n3) vs 60 k: 90 k -1.0 %,
+// 120 k -1.3 %, 180 k -0.9 %, 240 k +0.8 %
+#define AQ_TASKS_PER_JOB 120000
 #endif
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
 constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
@@ -724,7 +735,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
             shares_main = h;
-            D_main = seed_depth((unsigned long long)h * (unsigned long long)P.nshards);
+            D_main = seed_depth_job((unsigned long long)h * (unsigned long long)P.nshards);
         }
     }
     const unsigned W = gridDim.x * (unsigned)NW;
@@ -740,7 +751,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // (per-CU launches have no tail: k < 64)
     const unsigned tail_from = (!PCU && shares_main >= 8u) ? (unsigned)P.tail_from : (unsigned)P.nprob;
     const unsigned shares_tail = min(shares_main * (unsigned)P.tail_mult, W);
-    const int D_tail = seed_depth((unsigned long long)shares_tail * (unsigned long long)P.nshards);
+    const int D_tail = seed_depth_job((unsigned long long)shares_tail * (unsigned long long)P.nshards);
     const unsigned main_jobs = tail_from * shares_main;
     const unsigned total_jobs = main_jobs + ((unsigned)P.nprob - tail_from) * shares_tail;
     const unsigned base = wid * WCAP;                            // this wave's ring

@@ -58,6 +58,16 @@ def oracle():
     return pyoracle
 
 
+def device_seed_S(G, nshards):
+    """The seed depth offset S for oracle.integrate_shard() that reproduces the device's partition
+    (ppls_amd/csrc/aq_stream.h seed_depth / seed_depth_job): V = G * nshards, D = floor(log2 V) + 2,
+    one level deeper where (D + 2) levels x ceil(2^(D+1) / V) positions still fit 64 nodes."""
+    V = G * nshards
+    D = V.bit_length() - 1 + 2
+    nb = -(-(1 << (D + 1)) // V)
+    return 3 if (D + 2) * nb <= 64 else 2
+
+
 def exact_row(values, tasks=0, accepted=0, spilled=0, levels=0, error=0):
     """An exact row (include/aquad.h AQ_EXACT_ROW) of the given doubles, built with Python integers:
     limbs whose weighted sum is exactly sum(values) (the CPU shard backends of the dist tests)."""

@@ -8,6 +8,7 @@ import subprocess
 
 import numpy as np
 import pytest
+from conftest import device_seed_S
 
 pytestmark = pytest.mark.gpu
 
@@ -158,7 +159,8 @@ def test_shards_match_oracle_partition(ctx, trees, oracle, name, nshards):
     area = 0.0
     for s in range(nshards):
         r = ctx.integrate_shard(p, s, nshards)
-        o = oracle.integrate_shard(s, nshards, G=ctx.num_workers, S=2, integrand=p.integrand, a=p.a, b=p.b,
+        o = oracle.integrate_shard(s, nshards, G=ctx.num_workers, S=device_seed_S(ctx.num_workers, nshards),
+                                   integrand=p.integrand, a=p.a, b=p.b,
                                    eps=p.eps)
         assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
         assert r.tasks_per_level == o.tasks_per_level
@@ -435,7 +437,7 @@ def test_mixed_bounds_and_shards(ctx, oracle, trees):
     tot = [0, 0]
     for s in range(5):
         r = ctx.integrate_shard(_problem(g), s, 5)
-        o = oracle.integrate_shard(s, 5, G=ctx.num_workers, S=2, integrand=0, a=0.0, b=5.0, eps=1e-10)
+        o = oracle.integrate_shard(s, 5, G=ctx.num_workers, S=device_seed_S(ctx.num_workers, 5), integrand=0, a=0.0, b=5.0, eps=1e-10)
         assert (r.tasks, r.accepted) == (o.tasks, o.leaves)
         tot[0] += r.tasks
         tot[1] += r.accepted
@@ -625,7 +627,8 @@ def test_mixed_shard_launch(ctx, oracle, trees):
         ctx.set_level_histograms(True)
     want = {}
     for s in range(N):
-        o = oracle.integrate_shard(s, N, G=ctx.num_workers // (96 * N), S=2, integrand=1, a=1e-4, b=1.0, eps=1e-9)
+        G = ctx.num_workers // (96 * N)
+        o = oracle.integrate_shard(s, N, G=G, S=device_seed_S(G, N), integrand=1, a=1e-4, b=1.0, eps=1e-9)
         want[s] = (o.tasks, o.leaves)
     for i, s in enumerate(shards):
         assert (got[i].tasks, got[i].accepted) == want[int(s)], (i, int(s))

@@ -198,3 +198,15 @@ def test_deep_fixture_pinned_by_reference(deep_golden):
     assert r.tasks == g["tasks"] == g["reference"]["tasks_total"]
     assert (r.leaves, r.levels) == (g["leaves"], g["levels"])
     assert abs(float(g["reference"]["area_printed"]) - r.area) <= 5e-7 + 1e-12 * r.area
+
+
+def test_device_seed_depth_rule():
+    """tests' device_seed_S restates aq_stream.h seed_depth_job: one level deeper only where the
+    seeding's 64-node fast path holds it (the bench's adaptive jobs, whole-integral jobs), never for a
+    lone launch's 3072 shares or the sharded launches' 32 virtual workers."""
+    from conftest import device_seed_S
+    assert device_seed_S(3072, 1) == 2       # lone: 14 levels x 3 positions; deeper = 15 x 6 = 90 nodes
+    assert device_seed_S(3072, 2) == 2
+    assert device_seed_S(16, 2) == 2         # sharded multi-integral: V = 32, deeper = 9 x 8 = 72
+    assert device_seed_S(24, 1) == 3         # adaptive jobs: 8 levels x 6 = 48 nodes
+    assert device_seed_S(1, 1) == 3          # whole-integral jobs: 4 levels x 8 = 32 nodes
