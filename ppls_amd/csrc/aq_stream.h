@@ -188,7 +188,10 @@ static_assert((unsigned)MAXK - 1u <= TAG_MASK, "the tag field must hold every in
 constexpr int NPARTS = 65536;
 __host__ __device__ __forceinline__ size_t parts_row(int slot) { return slot < NPARTS ? (size_t)slot : (size_t)NPARTS; }
 #ifndef AQ_GSPLIT_DEFAULT
-#define AQ_GSPLIT_DEFAULT 96   // sharded launches / first launch: 32 shares per integral (2-rank rehearsal: 32 -> 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11)
+// sharded launches / first launch: 16 shares per integral over all shards (2-rank rehearsal, r03: 32 ->
+// 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11; r04 rank-0 launch of N x 16384 integrals sharded N ways,
+// profiles/r04n5/shard_ab.txt: 96 -> 192 = -2.0 / -3.8 / -4.0 % at N = 2 / 4 / 8, 384 worse at 8)
+#define AQ_GSPLIT_DEFAULT 192
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
 #ifndef AQ_LONE_GSPLIT

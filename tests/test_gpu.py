@@ -627,7 +627,7 @@ def test_mixed_shard_launch(ctx, oracle, trees):
         ctx.set_level_histograms(True)
     want = {}
     for s in range(N):
-        G = ctx.num_workers // (96 * N)
+        G = ctx.num_workers // (192 * N)   # aq_stream.h AQ_GSPLIT_DEFAULT waves per share and shard (V = 16: deeper seeding)
         o = oracle.integrate_shard(s, N, G=G, S=device_seed_S(G, N), integrand=1, a=1e-4, b=1.0, eps=1e-9)
         want[s] = (o.tasks, o.leaves)
     for i, s in enumerate(shards):
