@@ -189,8 +189,8 @@ constexpr int NPARTS = 65536;
 __host__ __device__ __forceinline__ size_t parts_row(int slot) { return slot < NPARTS ? (size_t)slot : (size_t)NPARTS; }
 #ifndef AQ_GSPLIT_DEFAULT
 // sharded launches / first launch: 16 shares per integral over all shards (2-rank rehearsal, r03: 32 ->
-// 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11; r04 rank-0 launch of N x 16384 integrals sharded N ways,
-// profiles/r04n5/shard_ab.txt: 96 -> 192 = -2.0 / -3.8 / -4.0 % at N = 2 / 4 / 8, 384 worse at 8)
+// 1.743e11, 64 -> 1.778e11, 96 -> 1.803e11; r04, per task of a launch of N x 16384 integrals sharded
+// N ways, profiles/r04n5/shard_ab.txt: 96 -> 192 = +1.3 / +0.3 / +0 % at N = 2 / 4 / 8, 384 -0.8 % at 8)
 #define AQ_GSPLIT_DEFAULT 192
 #endif
 constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's job = the share of this many waves
@@ -752,7 +752,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // idling behind the longest last job (each integral keeps ONE partition: the counts are exact)
     // (only where an integral is already several jobs: whole-integral jobs of tiny trees are short)
     // (per-CU launches have no tail: k < 64)
-    const unsigned tail_from = (!PCU && shares_main >= 8u) ? (unsigned)P.tail_from : (unsigned)P.nprob;
+    const unsigned tail_from = (!PCU && shares_main * (unsigned)P.nshards >= 8u) ? (unsigned)P.tail_from : (unsigned)P.nprob;
     const unsigned shares_tail = min(shares_main * (unsigned)P.tail_mult, W);
     const int D_tail = seed_depth_job((unsigned long long)shares_tail * (unsigned long long)P.nshards);
     const unsigned main_jobs = tail_from * shares_main;

@@ -452,6 +452,7 @@ def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
     a, b = oracle.batch_bounds(64)
     oa, ot, ol = oracle.integrate_batch(a, b, 1e-3)
     ctx.set_level_histograms(False)
+    phase_shard_checked = [False, False]
     try:
         for phase in ["big", "big", "small", "small", "big", "shard", "shard", "big"]:
             if phase == "big":
@@ -467,7 +468,19 @@ def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
                 tot = np.zeros((64, 2), np.int64)
                 for s in range(2):
                     ctx.integrate_many_async(np.zeros(64), np.full(64, 5.0), 1e-10, first_slot=0, shard=s, nshards=2)
-                    tot += np.array([(r.tasks, r.accepted) for r in (ctx.fetch(i) for i in range(64))], np.int64)
+                    rs = [ctx.fetch(i) for i in range(64)]
+                    tot += np.array([(r.tasks, r.accepted) for r in rs], np.int64)
+                    if phase_shard_checked[s]:
+                        continue
+                    phase_shard_checked[s] = True
+                    # each shard's partition against the oracle's: the launch's main integrals at
+                    # AQ_GSPLIT_DEFAULT (192) waves per share and shard, its last 64/32 = 2 integrals
+                    # (the tail, aq_abi.inc AQ_TAIL_DIV / AQ_TAIL_MULT) at 4x the shares
+                    Gm = ctx.num_workers // (192 * 2)
+                    for i, G in ((0, Gm), (63, min(4 * Gm, ctx.num_workers))):
+                        o = oracle.integrate_shard(s, 2, G=G, S=device_seed_S(G, 2), integrand=0, a=0.0, b=5.0,
+                                                   eps=1e-10)
+                        assert (rs[i].tasks, rs[i].accepted) == (o.tasks, o.leaves), (s, i)
                 assert (tot == np.array([g10["tasks"], g10["leaves"]])).all()
     finally:
         ctx.set_level_histograms(True)

@@ -23,7 +23,7 @@ def main():
     ctx = Context(0)
     ctx.set_level_histograms(False)
     out = {"k": args.k, "scale_k": args.scale_k}
-    base = None
+    base = base_tasks = None
     for n in [int(v) for v in args.shards.split(",")]:
         k = args.k * n if args.scale_k else args.k
         ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-10, shard=0, nshards=n)   # warmup
@@ -38,7 +38,13 @@ def main():
         r = ctx.fetch(0)
         if base is None:
             base = us
-        out[f"shards{n}"] = {"kernel_us": us, "tasks_rank0": r.tasks, "efficiency_vs_1": base / (n * us)}
+        if base_tasks is None:
+            base_tasks = r.tasks
+        # rank 0 holds shard 0 of every integral here (the bench rotates shards over ranks), and shard 0
+        # holds a little more or less than 1/N of each tree: the per-task rate is what the bench sees
+        share = r.tasks * n / base_tasks
+        out[f"shards{n}"] = {"kernel_us": us, "tasks_rank0": r.tasks, "rank0_task_share_x_n": share,
+                             "efficiency_vs_1": base / (n * us), "efficiency_per_task": base * share / (n * us)}
     print(json.dumps(out, indent=1))
 
 
