@@ -143,3 +143,15 @@ def test_integration_mpi_binding_compiles(tmp_path):
     c.write_text(src)
     subprocess.run(["gcc", "-Wall", "-Wextra", "-Werror", "-c", "-I/opt/conda/include", "-I", os.path.join(ROOT, "include"),
                     "-o", str(tmp_path / "b.o"), str(c)], check=True, capture_output=True, text=True, timeout=60)
+
+
+def test_oracle_seed_depth_rule_matches_library(lib):
+    """The oracle partition's seed depth (tests' device_seed_S: floor(log2 V) + S) equals the
+    library's own (aq_seed_depth = aq_stream.h seed_depth_job) for every V a launch can have."""
+    import ctypes
+    from conftest import device_seed_S
+    f = lib.aq_seed_depth
+    f.argtypes = [ctypes.c_ulonglong]
+    f.restype = ctypes.c_int
+    for V in list(range(1, 4097)) + [6144, 9216, 15360, 24576, 3072 * 16]:
+        assert f(V) == (V.bit_length() - 1) + device_seed_S(V, 1), V
