@@ -752,7 +752,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // idling behind the longest last job (each integral keeps ONE partition: the counts are exact)
     // (only where an integral is already several jobs: whole-integral jobs of tiny trees are short)
     // (per-CU launches have no tail: k < 64)
-    const unsigned tail_from = (!PCU && shares_main * (unsigned)P.nshards >= 8u) ? (unsigned)P.tail_from : (unsigned)P.nprob;
+    const unsigned tail_from = (!PCU && shares_main >= 8u) ? (unsigned)P.tail_from : (unsigned)P.nprob;
     const unsigned shares_tail = min(shares_main * (unsigned)P.tail_mult, W);
     const int D_tail = seed_depth_job((unsigned long long)shares_tail * (unsigned long long)P.nshards);
     const unsigned main_jobs = tail_from * shares_main;

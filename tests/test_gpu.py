@@ -473,11 +473,11 @@ def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
                     if phase_shard_checked[s]:
                         continue
                     phase_shard_checked[s] = True
-                    # each shard's partition against the oracle's: the launch's main integrals at
-                    # AQ_GSPLIT_DEFAULT (192) waves per share and shard, its last 64/32 = 2 integrals
-                    # (the tail, aq_abi.inc AQ_TAIL_DIV / AQ_TAIL_MULT) at 4x the shares
+                    # each shard's partition against the oracle's: every integral of a sharded launch
+                    # at AQ_GSPLIT_DEFAULT (192) waves per share and shard -- the last ones too (no
+                    # end-of-launch tail for shards: all shards of an integral share its partition)
                     Gm = ctx.num_workers // (192 * 2)
-                    for i, G in ((0, Gm), (63, min(4 * Gm, ctx.num_workers))):
+                    for i, G in ((0, Gm), (63, Gm)):
                         o = oracle.integrate_shard(s, 2, G=G, S=device_seed_S(G, 2), integrand=0, a=0.0, b=5.0,
                                                    eps=1e-10)
                         assert (rs[i].tasks, rs[i].accepted) == (o.tasks, o.leaves), (s, i)
