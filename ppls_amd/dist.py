@@ -62,6 +62,21 @@ def _agree_on_errors(code: int, dev, group) -> None:
         raise AquadError(f"rank {r} failed ({_lib.load().aq_strerror(c).decode() if c < 0 else 'error'}, code {c})", c)
 
 
+def _agree_on_workers(num_workers: int, dev, group) -> None:
+    """The shard partition (shares, seed depth) is a function of the persistent worker count, so every
+    rank must run the same one: ranks with different AQ_GRID settings or CU counts would combine shards
+    of different partitions into wrong counts with no error. One all-gather; a mismatch raises on
+    every rank (as aq_group does for the contexts of one process)."""
+    world = dist.get_world_size(group)
+    mine = torch.tensor([int(num_workers)], dtype=torch.int64, device=dev)
+    rows = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(rows, mine, group=group)
+    seen = [int(r.item()) for r in rows]
+    if len(set(seen)) != 1:
+        raise AquadError(f"ranks disagree on the persistent worker count {seen}: their shard partitions differ",
+                         -1)   # AQ_EINVAL
+
+
 def _err_code_from_bits(bits: int) -> int:
     """The C ABI's error code for a row's device error bits (aq_abi.inc err_from_bits)."""
     if bits & 1:
@@ -113,6 +128,8 @@ def integrate_distributed(problem: Problem, group=None, ctx: Optional[Context] =
         own = True
     dev = comm_device(group, ctx if shard_fn is None else None) if (nccl or shard_fn is None) else torch.device("cpu")
     row, err = np.zeros(ROW, np.int64), 0
+    if shard_fn is None:
+        _agree_on_workers(ctx.num_workers, dev, group)
     try:
         if shard_fn is None:
             row = ctx.integrate_shard_exact(problem, rank, world)   # internal slot: async slots untouched
@@ -206,6 +223,8 @@ def integrate_batch_distributed(a, b, eps, integrand=0, group=None, runner=None,
     dev = torch.device("cpu") if dist.get_backend(group) != "nccl" else torch.device("cuda", runner.ctx.device)
     if runner is None:
         raise AquadError("integrate_batch_distributed needs a runner (HipBatchRunner(ctx) on the GPU)")
+    if getattr(runner, "ctx", None) is not None:
+        _agree_on_workers(runner.ctx.num_workers, dev, group)
     total = np.zeros((n, ROW), np.int64)
     shard_cost = np.ones(S)               # cost model: mean measured tasks of shard index s
     seen = np.zeros(S)

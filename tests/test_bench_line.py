@@ -36,7 +36,7 @@ def _worker(rank, world, port, q):
         stats = bench.rank_stats(dist, "cpu", True, 40.0 + 4 * rank, 4, 1000.0 * (rank + 1), 0.05 + 0.01 * rank)
         args = argparse.Namespace(warmup=2, eps=1e-10)
         tot = np.array([[0.0, 1464273.0, 732137.0, 0.0]] * 8)
-        line = bench.bench_line(args, world, 8, 1, 8, 0.06, 8 * 732137.0, 8 * 1464275.0, tot, 8.0, 256, 0.0, 0,
+        line = bench.bench_line(args, world, 8, 1, 8, 0.06, 8 * 732137.0, 8 * 1464275.0, tot, 8.0, (256, 3072, 256), 0.0, 0,
                                 seen == world, dist.get_backend(), seen, stats, 1e12, 10.0, 8 * 1464273.0 / world,
                                 None)
         q.put((rank, line))
@@ -104,6 +104,7 @@ def test_launcher_spawns_n_ranks_after_the_cpu_baseline():
     assert "--nproc-per-node=2" in cmd and "--nnodes=1" in cmd and "127.0.0.1" in cmd
     assert cmd[-7:] == [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
     assert json.loads(env[bench.CPU_ENV]) == {"value": 1.0, "kind": "port", "eps": 1e-10}
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"   # the dmabuf IPC mode RCCL needs, set for the ranks
     # --no-cpu-baseline: nothing timed, nothing handed over
     calls.clear()
     order.clear()
@@ -151,3 +152,90 @@ def test_area_check():
     want = bench.GOLDEN[1e-10][2]
     assert bench.areas_ok([want, want * (1 + 5e-13)], want)
     assert not bench.areas_ok([want, want * (1 + 2e-12)], want)
+
+
+def _rotation_worker(rank, world, port, shard_tasks, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    try:
+        import bench
+        seen = bench.ranks_seen(dist, "cpu", True)
+        workers = bench.agree_on_workers(dist, "cpu", True, 3072)
+        K, B = 20, 32768
+        lb = max(1, min(world, (1 << 18) // B))          # bench.py: N batches per launch within 262144 slots
+        plan = bench.launch_plan(K, lb)
+        tasks = 0
+        for m in plan:
+            sh = bench.shard_rotation(rank, world, m * B)
+            tasks += int((np.bincount(sh, minlength=world) * np.asarray(shard_tasks, np.int64)).sum())
+        stats = bench.rank_stats(dist, "cpu", True, 1.0, len(plan), float(tasks), 0.1)
+        q.put((rank, seen, workers, plan, stats))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_rotation_balances_eight_ranks(oracle):
+    """VERDICT r4 #5c: the N = 8 launch pattern bench.py's driver run will use -- 20 timed steps of
+    32768 integrals as launches of 8 + 8 + 4 steps, each rank holding shard (rank + i) mod 8 of the
+    launch's i-th integral -- over a gloo group of 8 ranks on CPU, with every shard's task count from
+    the oracle's restatement of the device partition (16 virtual workers: 2 shares x 8 shards,
+    tests/conftest.py device_seed_S). The ranks' tasks must be equal (imbalance <= 1.01) and sum to
+    the 20 x 32768 whole trees; the snake partition's raw per-shard skew is kept in the assertion."""
+    from conftest import device_seed_S
+    world = 8
+    G = 3072 // (192 * world)          # aq_stream.h AQ_GSPLIT_DEFAULT waves per share and shard
+    shard_tasks = [oracle.integrate_shard(s, world, G=G, S=device_seed_S(G, world), eps=1e-10).tasks
+                   for s in range(world)]
+    total = 1464273
+    assert sum(shard_tasks) == total
+    assert max(shard_tasks) / (total / world) > 1.005   # the skew the rotation has to cancel
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rotation_worker, args=(r, world, port, shard_tasks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen, workers, plan, stats = got[0]
+    assert seen == world and workers == [3072] * world
+    assert plan == [8, 8, 4]
+    assert stats["task_imbalance"] <= 1.01
+    assert sum(stats["tasks"]) == 20 * 32768 * total
+    assert all(got[r][3] == stats for r in range(world))   # every rank holds the same gathered view
+
+
+def _workers_mismatch(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    try:
+        import bench
+        try:
+            bench.agree_on_workers(dist, "cpu", True, 3072 if rank == 0 else 2048)
+            q.put((rank, "agreed"))
+        except SystemExit as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ranks_with_different_partitions_fail():
+    """ranks whose persistent worker counts differ (AQ_GRID, CU count) would combine shards
+    of different partitions; bench.py's check fails on every rank instead."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_workers_mismatch, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all("disagree" in got[r] for r in range(world))

@@ -203,3 +203,29 @@ def test_gloo_batch_error_bits_raise_everywhere():
     healthy ranks must not be left in the all-reduce."""
     results = _run(_bits_worker, 2, timeout=120)
     assert all("rank 1 failed" in results[r] and "depth" in results[r] for r in range(2)), results
+
+
+def _workers_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        import types
+        from ppls_amd.aquad import AquadError
+        from ppls_amd.dist import integrate_batch_distributed
+        runner = _OracleBatchRunner()
+        runner.ctx = types.SimpleNamespace(num_workers=3072 if rank == 0 else 2048)   # e.g. AQ_GRID on rank 1
+        try:
+            integrate_batch_distributed(np.full(4, 1e-4), np.ones(4), 1e-5, integrand=1, runner=runner,
+                                        shards_per_integral=2, window=4, rebalance=False)
+            q.put((rank, "no error"))
+        except AquadError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_batch_ranks_on_different_partitions_raise():
+    """the shard partition follows the persistent worker count; ranks that disagree on it
+    (AQ_GRID, CU counts) raise together before any shard runs, instead of combining shards of
+    different partitions into wrong counts."""
+    results = _run(_workers_worker, 2, timeout=120)
+    assert all("disagree" in results[r] for r in range(2)), results

@@ -50,6 +50,26 @@
                  : "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]),    \
                    "+v"(a[14]), "+v"(a[15]));
 
+// 64-bit shift-add with a constant shift (the round's dt + 1)
+#define R16_SH(OP)                                                                              \
+    asm volatile(OP " %0, %0, 0, %0\n" OP " %1, %1, 0, %1\n" OP " %2, %2, 0, %2\n" OP " %3, %3, 0, %3\n" \
+                 OP " %4, %4, 0, %4\n" OP " %5, %5, 0, %5\n" OP " %6, %6, 0, %6\n" OP " %7, %7, 0, %7\n" \
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),        \
+                   "+v"(a[6]), "+v"(a[7]));                                                       \
+    asm volatile(OP " %0, %0, 0, %0\n" OP " %1, %1, 0, %1\n" OP " %2, %2, 0, %2\n" OP " %3, %3, 0, %3\n" \
+                 OP " %4, %4, 0, %4\n" OP " %5, %5, 0, %5\n" OP " %6, %6, 0, %6\n" OP " %7, %7, 0, %7\n" \
+                 : "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]),    \
+                   "+v"(a[14]), "+v"(a[15]));
+
+// VOPC: compares writing vcc (independent sources, one destination)
+#define R16_CMP(OP)                                                                             \
+    asm volatile(OP " %0, %1\n" OP " %1, %2\n" OP " %2, %3\n" OP " %3, %4\n"                     \
+                 OP " %4, %5\n" OP " %5, %6\n" OP " %6, %7\n" OP " %7, %0\n"                     \
+                 OP " %0, %1\n" OP " %1, %2\n" OP " %2, %3\n" OP " %3, %4\n"                     \
+                 OP " %4, %5\n" OP " %5, %6\n" OP " %6, %7\n" OP " %7, %0\n"                     \
+                 :: "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]),    \
+                   "v"(a[7]) : "vcc");
+
 template <int OPID, typename T>
 __global__ void __launch_bounds__(256) k_issue(T* out, int iters) {
     T a[16];
@@ -65,6 +85,13 @@ __global__ void __launch_bounds__(256) k_issue(T* out, int iters) {
         else if constexpr (OPID == 6) { R16_2("v_max_f64") }
         else if constexpr (OPID == 7) { R16("v_frexp_mant_f64") }
         else if constexpr (OPID == 9) { R16_3("v_fma_f32") }
+        else if constexpr (OPID == 10) { R16("v_mov_b64") }
+        else if constexpr (OPID == 11) { R16_3("v_and_or_b32") }
+        else if constexpr (OPID == 12) { R16_2("v_mbcnt_lo_u32_b32") }
+        else if constexpr (OPID == 13) { R16_3("v_lshl_add_u32") }
+        else if constexpr (OPID == 14) { R16_SH("v_lshl_add_u64") }
+        else if constexpr (OPID == 15) { R16_CMP("v_cmp_gt_f64_e32 vcc,") }
+        else if constexpr (OPID == 16) { R16_2("v_cndmask_b32") }
     }
     T s = 0;
 #pragma unroll
@@ -102,7 +129,7 @@ int main() {
     double* d;
     CHECK(hipMalloc(&d, sizeof(double) * 256 * 256 * 8));
     float* f = (float*)d;
-    for (int w : {1, 2, 4}) {
+    for (int w : {1, 2, 3, 4}) {
         run<0>("v_fma_f64", d, w);
         run<1>("v_mul_f64", d, w);
         run<2>("v_add_f64", d, w);
@@ -112,6 +139,13 @@ int main() {
         run<5, float>("v_rcp_f32", f, w);
         run<9, float>("v_fma_f32", f, w);
         run<6, double>("v_max_f64", d, w);
+        run<10, double>("v_mov_b64", d, w);
+        run<11, float>("v_and_or_b32", f, w);
+        run<12, float>("v_mbcnt_lo_u32_b32", f, w);
+        run<13, float>("v_lshl_add_u32", f, w);
+        run<14, double>("v_lshl_add_u64", d, w);
+        run<15, double>("v_cmp_gt_f64", d, w);
+        run<16, float>("v_cndmask_b32", f, w);
     }
     CHECK(hipFree(d));
     return 0;
