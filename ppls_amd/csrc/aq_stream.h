@@ -74,6 +74,14 @@ constexpr int S_W = AQ_S_W;              // seed depth D = floor(log2 V) + S_W: 
 #define AQ_JOB_RUN_MAX 16
 #endif
 constexpr int JOB_RUN_MAX = AQ_JOB_RUN_MAX;   // most jobs one claim takes (whole-integral jobs only)
+#ifndef AQ_GSS_DIV
+#define AQ_GSS_DIV 2
+#endif
+// Guided claims (r05): a claimed run holds min(JOB_RUN_MAX, jobs left / (GSS_DIV x W)) jobs, so the runs
+// shrink to one job as the counter nears the end and the waves run dry together. With fixed runs of 16
+// tiny jobs (C3 at eps=1e-3: ~1 400 tasks, ~20 us each) the last runs claimed held the launch ~0.1-0.3
+// ms past the others (DIAG: last rounds spread over ~100 us of a 512 us launch, profiles/r05a).
+constexpr unsigned GSS_DIV = AQ_GSS_DIV;
 #ifndef AQ_S_W1
 #define AQ_S_W1 2
 #endif
@@ -290,6 +298,9 @@ struct alignas(128) SlotSums {
     unsigned levels, error;
     unsigned pcu;       // 1: a per-CU launch wrote this slot's counts as per-workgroup words (parts),
                         // not into tasks / leaves / levels -- readers add them (slot_counts)
+    unsigned win_lo_not, win_hi;   // the area limbs ever added to: [~win_lo_not, win_hi), both folded by
+                                   // max (aq_xsum.h xs_win_lo / xs_win_hi; 0 / 0 = none) -- the batch
+                                   // gather reads and re-zeroes only these (k_gather_reset)
 };
 // Per-integral totals and histogram accumulators, one per async slot; all-zero when a launch starts
 // (the host zeroes used slots lazily, in batches).
@@ -323,13 +334,22 @@ __host__ __device__ __forceinline__ Counts slot_counts(const SlotSums& sm, const
     return c;
 }
 
-// Exact accumulation into a slot's XSum (device atomics: any order, same bits).
-__device__ __forceinline__ void xs_atomic_add(long long* limbs, double x) {
+// Exact accumulation into a slot's XSum (device atomics: any order, same bits). Returns the first limb
+// the value's digits touch (three from there), or -1 for x == 0.
+__device__ __forceinline__ int xs_atomic_add(long long* limbs, double x) {
     XDigits g;
-    if (!xs_digits(x, g)) return;
+    if (!xs_digits(x, g)) return -1;
 #pragma unroll
     for (int k = 0; k < 3; ++k)
         if (g.d[k]) atomicAdd(reinterpret_cast<unsigned long long*>(&limbs[g.i + k]), (unsigned long long)g.d[k]);
+    return g.i;
+}
+// ... and widen the slot's limb window to cover limbs i .. i + 2 of each (i >= 0) add
+__device__ __forceinline__ void xs_window_add(SlotSums& sm, int i0, int i1) {
+    const int lo = i0 < 0 ? i1 : (i1 < 0 ? i0 : min(i0, i1)), hi = max(i0, i1);
+    if (lo < 0) return;
+    atomicMax(&sm.win_lo_not, xs_win_lo(lo));
+    atomicMax(&sm.win_hi, xs_win_hi(hi));
 }
 
 struct Chunk {                      // SoA, one queue slot
@@ -411,7 +431,7 @@ enum : int {
     DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
     DG_SEED_CALLS, DG_FLUSHES, DG_MIXED_ROUNDS, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_CELLAR_IN,
     DG_CELLAR_OUT, DG_C_REFILL, DG_C_LOOP, DG_ACTIVE_TASKS, DG_PREFETCH, DG_T_INIT, DG_T_DONE, DG_T_FOLD,
-    DG_T_BROKE, DG_T_FLUSHED, DG_C_P1_CLASS, DG_C_P1_WALK, DG_C_P1_F, DG_T_SEED_IN, DG_T_CLASS, DG_PAD47,
+    DG_T_BROKE, DG_T_FLUSHED, DG_C_P1_CLASS, DG_C_P1_WALK, DG_C_P1_F, DG_T_SEED_IN, DG_T_CLASS, DG_POLLS,
     DIAG_WORDS = 48
 };
 
@@ -529,8 +549,9 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
                 atomicAdd(&c.sums.tasks, (unsigned long long)t);
                 atomicAdd(&c.sums.leaves, (unsigned long long)l);
                 atomicMax(&c.sums.levels, m);
-                xs_atomic_add(c.area.limb, hi);
-                xs_atomic_add(c.area.limb, lo);
+                const int i0 = xs_atomic_add(c.area.limb, hi);
+                const int i1 = xs_atomic_add(c.area.limb, lo);
+                xs_window_add(c.sums, i0, i1);
             }
         }
     }
@@ -657,8 +678,13 @@ __device__ __forceinline__ unsigned ring_wrap(unsigned v) {
 __device__ unsigned long long g_aq_stamps[MAXG * NW * ST_STRIDE];
 #endif
 
-template <int FID, bool HIST, bool DIAG, bool PCU>
-__global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
+// NWT: waves per workgroup -- NW (12: three per SIMD) for every launch but the unsharded lone ones,
+// which run AQ_LONE_NW (aq_abi.inc launch_stream): a lone integral's set-up and seeding are VALU-bound
+// at three waves per SIMD, and its rounds are bound by one wave's heaviest share.
+template <int FID, bool HIST, bool DIAG, bool PCU, int NWT = NW>
+__global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
+    constexpr int PTT = NWT * 64;   // threads per workgroup
+    static_assert(NWT >= 4 && NWT <= NW && NWT % 4 == 0, "whole waves per SIMD, within the LDS rings");
     // one SoA block (a | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
     // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
     // pair stores no midpoint: m = (a + b) / 2 is recomputed with the parent's own operands (:187),
@@ -702,21 +728,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     // CU had cost every launch 0.75 us, r04j)
     ExpPair tv{};
     if (FID != F_SIN_RECIP && tid < 128u) tv = reinterpret_cast<const ExpPair*>(kExpTabBits)[tid];
-    static_assert(AQ_SINCOS_TAB_N <= PT, "one sin-table entry per thread");
+    static_assert(FID != F_SIN_RECIP || AQ_SINCOS_TAB_N <= PTT, "one sin-table entry per thread");
     double sv = 0.0;
     if (FID == F_SIN_RECIP && tid < (unsigned)AQ_SINCOS_TAB_N) sv = kSinCosTab[tid];
     stamp(ST_PRE);
     if (bid == 0)
-        for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
+        for (unsigned i = tid; i < (unsigned)(sizeof(QCtl) / 4); i += PTT) reinterpret_cast<unsigned*>(P.q_next)[i] = 0u;
     if (tid == 0) {
         S.lock = 0; S.pbot = 0; S.ptop = 0; S.idle = 0; S.phase = 0; S.busy_token = 1;
         S.exited = 0; S.tasks = 0;
     }
     if (PCU && tid < 3u * PCU_ROW) s_pc[tid] = 0ull;
     if (PCU)
-        for (unsigned i = tid; i < (unsigned)(PCU_ROW * XS_LIMBS); i += PT) s_px[i / XS_LIMBS].limb[i % XS_LIMBS] = 0;
+        for (unsigned i = tid; i < (unsigned)(PCU_ROW * XS_LIMBS); i += PTT) s_px[i / XS_LIMBS].limb[i % XS_LIMBS] = 0;
     if (DIAG) {
-        for (unsigned i = tid; i < DIAG_WORDS; i += PT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
+        for (unsigned i = tid; i < DIAG_WORDS; i += PTT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
     if (FID == F_SIN_RECIP) {
         if (tid < (unsigned)AQ_SINCOS_TAB_N) reinterpret_cast<double*>(tab)[tid] = sv;
@@ -741,8 +767,8 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             D_main = seed_depth_job((unsigned long long)h * (unsigned long long)P.nshards);
         }
     }
-    const unsigned W = gridDim.x * (unsigned)NW;
-    const unsigned w_all = bid * (unsigned)NW + wid;
+    const unsigned W = gridDim.x * (unsigned)NWT;
+    const unsigned w_all = bid * (unsigned)NWT + wid;
     // termination group (QCtl): its workgroup count, and T0 = the number of groups
     const unsigned grp = bid % (unsigned)NGROUP;
     const unsigned grp_size = (gridDim.x - grp + (unsigned)NGROUP - 1u) / (unsigned)NGROUP;
@@ -785,6 +811,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                              ? max(1u, min((unsigned)JOB_RUN_MAX, total_jobs / (4u * W)))
                              : 1u;
     unsigned job_end = job + 1u;  // end of the claimed run `job` belongs to
+    unsigned claim_n = jpc;       // jobs the claim in flight takes (guided: shrinks near the end)
     unsigned err = 0;
     bool mixed = false;           // a round met pairs of another integral (never expected)
     unsigned top = 0, bot = 0;    // ring indices (wave-uniform)
@@ -799,7 +826,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
     constexpr unsigned give_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE : (unsigned)GIVE_ROUNDS;
     constexpr unsigned poll_rounds = FID == F_SIN_RECIP ? (unsigned)SKEWED_POLL : (unsigned)POLL_ROUNDS;
     constexpr unsigned give_min = FID == F_SIN_RECIP ? (unsigned)SKEWED_GIVE_MIN : (unsigned)GIVE_MIN;
-    unsigned poll_ctr = wid * (poll_rounds / NW);
+    unsigned poll_ctr = wid * (poll_rounds / NWT);
     unsigned seen_head = 0, seen_tail = 0;   // lane 0's view of the HBM queue
     unsigned long long spilled = 0;          // pairs this wave sent to HBM chunks (lane 0)
     unsigned long long lock_spins = 0;
@@ -887,8 +914,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
             if (job_pending) {
                 job = W + uni(__shfl(claim, 0, 64));   // claims count from W (the first W jobs are dealt)
-                job_end = job + jpc;
+                job_end = job + claim_n;
                 job_pending = false;
+
             }
             unsigned k = 0;
             int ptag = 0;
@@ -915,7 +943,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 if (lane == 0) old = __hip_atomic_fetch_add(&S.idle, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 old = uni(__shfl(old, 0, 64));
                 counted_idle = true;
-                counted_now = old + 1u != (unsigned)NW;
+                counted_now = old + 1u != (unsigned)NWT;
             }
             if (!seed && !counted_now) {
                 wave_lock(&S.lock, lane, lock_spins);
@@ -954,7 +982,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                             counted_idle = true;
                         }
                         __builtin_amdgcn_wave_barrier();
-                        if (phase == 0 && uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == NW) {   // every wave idle, pool empty, nothing to seed
+                        if (phase == 0 && uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == NWT) {   // every wave idle, pool empty, nothing to seed
                             lead = true;
                             if (lane == 0) S.phase = 1;
                             __builtin_amdgcn_wave_barrier();
@@ -1044,7 +1072,10 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                     } else {
                         // next run: the latency hides behind this job. The raw counter value is kept (W is
                         // added at the read): any arithmetic on the result here would wait for the atomic
-                        if (lane == 0) claim = g_add(&qc->jobs.v, jpc);
+                        // guided size: the jobs left past this one, over GSS_DIV claims per wave
+                        const unsigned left = total_jobs > job + 1u ? total_jobs - job - 1u : 0u;
+                        claim_n = jpc > 1u && GSS_DIV ? max(1u, min(jpc, left / (GSS_DIV * W))) : jpc;   // (0: fixed runs)
+                        if (lane == 0) claim = g_add(&qc->jobs.v, claim_n);
                         job_pending = true;
                     }
                 } else {
@@ -1523,37 +1554,21 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         }
 
         ++poll_ctr;
-        // ---- feed idle sibling waves
-        if ((poll_ctr % give_rounds) == 0 && size >= give_min &&
-            uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) > 0 &&
-            uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
-                uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
-            const unsigned k = size / 2u;   // <= WCAP / 2 <= PCAP
-            wave_lock(&S.lock, lane, lock_spins);
-            const unsigned pt = uni(S.ptop);
-            const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
-            if (fits) {
-                for (unsigned i = lane; i < k; i += 64)
-                    copy_pair(R, base + ring_slot(bot + i), POOL0 + ((pt + i) & (PCAP - 1)));
-                if (lane == 0) S.ptop = pt + k;
-            }
-            wave_unlock(&S.lock, lane);
-            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_GIVE], (unsigned long long)(fits ? k : 0u)); }
-            if (fits) {
-                bot += k;
-                __builtin_amdgcn_wave_barrier();
-                continue;
-            }
-        }
-        // ---- donate to starving workgroups (another CU waits on the HBM queue)
+        // ---- donate to starving workgroups (another CU waits on the HBM queue). Checked before the
+        //      sibling give: every poll round is also a give round, and a successful give `continue`s
+        //      past the poll (r05: a CU whose waves keep feeding each other then never serves a waiting
+        //      one; DIAG of a 262144-integral tiny-tree launch, profiles/r05f-g)
         if ((poll_ctr % poll_rounds) == 0) {
             unsigned slot = 0xffffffffu;
             if (lane == 0) {
+                if constexpr (DIAG) atomicAdd(&s_dg[DG_POLLS], 1ull);   // polls (low word) | polls that saw a
+                                                                          // waiting ticket (high word)
                 if ((int)(seen_head - seen_tail) > 0) {
                     unsigned expect = seen_tail;
                     if (__hip_atomic_compare_exchange_strong(&qc->tail.v, &expect, seen_tail + 1u, __ATOMIC_RELAXED,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                         slot = seen_tail;
+                    if constexpr (DIAG) atomicAdd(&s_dg[DG_POLLS], 1ull << 32);
                 }
                 seen_head = g_ld(&qc->head.v);
                 seen_tail = g_ld(&qc->tail.v);
@@ -1594,6 +1609,28 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
             }
         }
 
+        // ---- feed idle sibling waves
+        if ((poll_ctr % give_rounds) == 0 && size >= give_min &&
+            uni(__hip_atomic_load(&S.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) > 0 &&
+            uni(__hip_atomic_load(&S.ptop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                uni(__hip_atomic_load(&S.pbot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+            const unsigned k = size / 2u;   // <= WCAP / 2 <= PCAP
+            wave_lock(&S.lock, lane, lock_spins);
+            const unsigned pt = uni(S.ptop);
+            const bool fits = (pt - S.pbot) + k <= (unsigned)PCAP;
+            if (fits) {
+                for (unsigned i = lane; i < k; i += 64)
+                    copy_pair(R, base + ring_slot(bot + i), POOL0 + ((pt + i) & (PCAP - 1)));
+                if (lane == 0) S.ptop = pt + k;
+            }
+            wave_unlock(&S.lock, lane);
+            if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_GIVE], (unsigned long long)(fits ? k : 0u)); }
+            if (fits) {
+                bot += k;
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
+        }
         // ---- running low: fetch the next 64 cellar pairs now, land them next iteration
         if (ctop > 0 && pf_n == 0 && size <= (unsigned)PF_ISSUE) {
             pf_n = 64u;   // ctop is a whole number of chunks
@@ -1827,7 +1864,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         // workgroup's tasks, the last workgroup sets shares per integral for ~TASKS_PER_JOB per job
         // (every launch: the workgroup's tasks also go to the context's per-CU counters, below)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // this wave's LDS flushes precede its exit count
-        const bool last = atomicAdd(&S.exited, 1u) == (unsigned)NW - 1u;
+        const bool last = atomicAdd(&S.exited, 1u) == (unsigned)NWT - 1u;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         last_u = last ? 1u : 0u;
         if (last) {
@@ -1848,7 +1885,12 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                 unsigned long long* wp = P.parts + 2 * ((size_t)p * gridDim.x + bid);
                 wp[0] = pack_cu(t, cu);
                 wp[1] = (l << 8) | (unsigned long long)(m & 255u);
-                if (bid == 0) P.ctls[P.first_slot + p].sums.pcu = 1u;
+                if (bid == 0) {
+                    SlotSums& sm = P.ctls[P.first_slot + p].sums;
+                    sm.pcu = 1u;
+                    sm.win_lo_not = xs_win_lo(0);   // per-CU slots: the full limb window (a few slots only)
+                    sm.win_hi = (unsigned)XS_LIMBS;
+                }
             }
         }
         if (!PCU && last && (P.adaptive & 2)) {
@@ -1877,6 +1919,9 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&g[i]), (unsigned long long)v);
                 }
+                // (the slot's limb window is the whole accumulator, stored once below by workgroup 0: 256
+                // workgroups folding two more atomics each into the sums line at the launch's end had
+                // cost a lone integral ~3 us, profiles/r05d)
             }
         }
     }
@@ -1887,7 +1932,7 @@ __global__ __launch_bounds__(PT) void k_stream(StreamParams P) {
         if (lane < (unsigned)ST_N) {   // vector stores, one word per lane
             unsigned long long v = 0;
             for (int i = 0; i < ST_N; ++i) v = lane == (unsigned)i ? stp[i] : v;
-            g_aq_stamps[(size_t)(bid * (unsigned)NW + wid) * ST_STRIDE + lane] = v;
+            g_aq_stamps[(size_t)(bid * (unsigned)NWT + wid) * ST_STRIDE + lane] = v;
         }
     }
 #endif

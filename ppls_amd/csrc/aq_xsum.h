@@ -75,22 +75,26 @@ AQ_HD void xs_add_xs(XSum& a, const XSum& b) {
     for (int i = 0; i < XS_LIMBS; ++i) a.limb[i] += b.limb[i];
 }
 
-// Correctly rounded (round-to-nearest-even) double of the exact sum.
-AQ_HD double xs_round(const XSum& a) {
+// Correctly rounded (round-to-nearest-even) double of the exact sum of n <= N limbs, limb 0 weighing
+// 2^e0: the whole accumulator (N = n = XS_LIMBS, e0 = XS_E0), or a window of it that holds every
+// nonzero limb (the batch gather reads only a slot's touched limbs: SlotSums' limb window) -- the
+// value, and so its rounding, does not depend on the zero limbs around the window.
+template <int N>
+AQ_HD double xs_round_span(const long long* limb, int n, int e0) {
     // carry-propagate into base-2^32 digits of the two's complement value
-    uint32_t dg[XS_LIMBS + 2];
+    uint32_t dg[N + 2];
     long long carry = 0;
-    for (int i = 0; i < XS_LIMBS; ++i) {
+    for (int i = 0; i < n; ++i) {
         // v = limb + carry cannot overflow: |limb| < 2^63 - 2^33 by the addition budget, |carry| < 2^32
-        const long long v = a.limb[i] + carry;
+        const long long v = limb[i] + carry;
         dg[i] = (uint32_t)((unsigned long long)v & 0xffffffffull);
         carry = v >> 32;                   // arithmetic shift: floor division
     }
     // carry is now the sign extension (0 or -1 for any representable total)
     const bool neg = carry < 0;
-    dg[XS_LIMBS] = (uint32_t)carry;
-    dg[XS_LIMBS + 1] = (uint32_t)(carry >> 32);
-    const int nd = XS_LIMBS + 2;
+    dg[n] = (uint32_t)carry;
+    dg[n + 1] = (uint32_t)(carry >> 32);
+    const int nd = n + 2;
     if (neg) {   // magnitude = two's complement negation
         unsigned long long c = 1;
         for (int i = 0; i < nd; ++i) {
@@ -105,7 +109,7 @@ AQ_HD double xs_round(const XSum& a) {
     int lz = 0;
     for (uint32_t v = dg[t]; !(v & 0x80000000u); v <<= 1) ++lz;
     const int b = 32 * t + 31 - lz;        // bit index of the leading one
-    const int e = b + XS_E0;               // its binary exponent
+    const int e = b + e0;               // its binary exponent
     if (e > 1023) return neg ? -__builtin_inf() : __builtin_inf();
     int keep = 53;
     if (e < -1022) keep = e + 1075;        // subnormal: bits down to 2^-1074 (>= 1: the sum is a multiple of 2^-1074)
@@ -122,7 +126,7 @@ AQ_HD double xs_round(const XSum& a) {
         for (int j = w - 1; j >= 0 && !sticky; --j) sticky = dg[j] != 0u;
     }
     if (rb && (sticky || (M & 1ull))) ++M;
-    int ex = low + XS_E0;                  // M * 2^ex
+    int ex = low + e0;                  // M * 2^ex
     if (M >> keep) {                       // rounding carried into a new bit
         M >>= 1;
         ++ex;
@@ -140,5 +144,12 @@ AQ_HD double xs_round(const XSum& a) {
     r = r * pow2(ex1) * pow2(ex2);
     return neg ? -r : r;
 }
+
+AQ_HD double xs_round(const XSum& a) { return xs_round_span<XS_LIMBS>(a.limb, XS_LIMBS, XS_E0); }
+
+// The limbs a value's digits touch, as a window [lo, hi) folded by max (so an all-zero pair of words
+// is the empty window): lo_not = ~lo, hi = last + 1. Kept per slot beside its sums.
+AQ_HD unsigned xs_win_lo(int i) { return ~(unsigned)i; }
+AQ_HD unsigned xs_win_hi(int i) { return (unsigned)i + 3u; }
 
 }  // namespace aq

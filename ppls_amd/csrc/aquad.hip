@@ -497,6 +497,43 @@ __global__ __launch_bounds__(64) void k_gather(const Ctl* __restrict__ ctls, con
     o[3] = (double)c.sums.error;
 }
 
+// The batch front end's gather (aq_integrate_batch): k_gather's rows, then every slot back to the
+// all-zero state the next launch needs -- its sums and the limbs of its window, the only ones any flush
+// added to (SlotSums win_lo_not / win_hi) -- so no k_reset runs before the next chunk's launch on the
+// same slots, and only a slot's touched lines are read and written (k_gather + k_reset read and wrote
+// all 68 limbs of every slot: 115 + 76 us per 262144-slot chunk, profiles/r05a/c3_timeline_r04code.json).
+constexpr int GATHER_WIN = 16;   // limbs a window may span to take the short path (a cosh4 tree: ~4-6)
+__global__ __launch_bounds__(64) void k_gather_reset(Ctl* __restrict__ ctls, const unsigned long long* __restrict__ parts,
+                                                     int grid, int first, int n, double* __restrict__ out) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const int slot = first + i;
+    Ctl& c = ctls[slot];
+    const SlotSums sm = c.sums;
+    const Counts k = slot_counts(sm, parts + 2 * parts_row(slot) * grid, grid);
+    const int lo = sm.win_hi ? (int)~sm.win_lo_not : 0;
+    const int hi = sm.win_hi ? min((int)sm.win_hi, XS_LIMBS) : 0;
+    double area;
+    if (hi - lo <= GATHER_WIN) {
+        long long w[GATHER_WIN];
+#pragma unroll
+        for (int j = 0; j < GATHER_WIN; ++j) w[j] = lo + j < hi ? c.area.limb[lo + j] : 0ll;
+        area = xs_round_span<GATHER_WIN>(w, hi - lo, XS_E0 + 32 * lo);
+#pragma unroll
+        for (int j = 0; j < GATHER_WIN; ++j)
+            if (lo + j < hi) c.area.limb[lo + j] = 0ll;
+    } else {
+        area = xs_round(c.area);
+        for (int j = 0; j < XS_LIMBS; ++j) c.area.limb[j] = 0ll;
+    }
+    double* o = out + 4 * (size_t)i;
+    o[0] = area;
+    o[1] = (double)k.tasks;
+    o[2] = (double)k.leaves;
+    o[3] = (double)sm.error;
+    c.sums = SlotSums{};
+}
+
 // The same slots as exact int64 rows (AQ_EXACT_ROW each): limbs, tasks, accepted, spilled,
 // levels | error << 32. Sums of such rows (an int64 all-reduce) keep the area exact.
 __global__ __launch_bounds__(64) void k_gather_exact(const Ctl* __restrict__ ctls,

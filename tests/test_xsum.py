@@ -13,6 +13,7 @@ import pytest
 from conftest import ROOT
 
 SRC = r"""
+#include <algorithm>
 #include "aq_xsum.h"
 extern "C" double xs_sum(const double* x, long n) {
     aq::XSum a;
@@ -27,6 +28,27 @@ extern "C" double xs_sum_split(const double* x, long n, int k) {
     for (long i = 0; i < n; ++i) aq::xs_add(acc[i % k], x[i]);
     for (int j = 1; j < k; ++j) aq::xs_add_xs(acc[0], acc[j]);
     return aq::xs_round(acc[0]);
+}
+// the batch gather's path (aquad.hip k_gather_reset): only the limb window the adds touched
+// (SlotSums win_lo_not / win_hi, folded by max), rounded with xs_round_span<16> when it spans <= 16
+// limbs; -1 in *used when the window was too wide (the full xs_round path)
+extern "C" double xs_sum_window(const double* x, long n, int* used) {
+    aq::XSum a;
+    memset(&a, 0, sizeof(a));
+    unsigned lo_not = 0, hi = 0;
+    for (long i = 0; i < n; ++i) {
+        aq::XDigits g;
+        if (!aq::xs_digits(x[i], g)) continue;
+        aq::xs_add(a, x[i]);
+        lo_not = std::max(lo_not, aq::xs_win_lo(g.i));
+        hi = std::max(hi, aq::xs_win_hi(g.i));
+    }
+    const int l = hi ? (int)~lo_not : 0, h = hi ? (int)hi : 0;
+    if (h - l > 16) { *used = -1; return aq::xs_round(a); }
+    *used = h - l;
+    for (int i = 0; i < aq::XS_LIMBS; ++i)
+        if ((i < l || i >= h) && a.limb[i] != 0) return -12345.0;   // a nonzero limb outside the window
+    return aq::xs_round_span<16>(a.limb + l, h - l, aq::XS_E0 + 32 * l);
 }
 """
 
@@ -46,9 +68,15 @@ def xs(tmp_path_factory):
     L.xs_sum_split.argtypes = [dp, ctypes.c_long, ctypes.c_int]
     L.xs_sum_split.restype = ctypes.c_double
 
+    L.xs_sum_window.argtypes = [dp, ctypes.c_long, ctypes.POINTER(ctypes.c_int)]
+    L.xs_sum_window.restype = ctypes.c_double
+
     def run(x, k=1):
         x = np.ascontiguousarray(x, np.float64)
         p = x.ctypes.data_as(dp)
+        if k == "window":
+            used = ctypes.c_int(0)
+            return L.xs_sum_window(p, x.size, ctypes.byref(used)), used.value
         return L.xs_sum(p, x.size) if k == 1 else L.xs_sum_split(p, x.size, k)
     return run
 
@@ -90,3 +118,24 @@ def test_subnormal_results(xs):
     x = rng.integers(-2 ** 40, 2 ** 40, 200) * 5e-324
     x = np.concatenate([x, [2.0 ** -1022, -2.0 ** -1022 + 5e-324]])
     assert same(xs(x), math.fsum(x.tolist()))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_window_rounding_matches_fsum(xs, seed):
+    """The batch gather rounds only a slot's limb window (r05): the same correctly rounded sum, on
+    quadrature-like partials (a narrow window: the short path) and on wide or cancelling ones (the
+    full-accumulator fallback above 16 limbs)."""
+    rng = np.random.default_rng(100 + seed)
+    n = 4000
+    if seed % 3 == 0:    # double-double partials of one integral: hi ~ 1e5, lo ~ 1e-12 of it
+        hi = rng.uniform(1e4, 1e6, n)
+        x = np.concatenate([hi, hi * rng.uniform(-1e-16, 1e-16, n)])
+    elif seed % 3 == 1:  # ties and cancellation inside a narrow range
+        base = rng.uniform(1, 2, n)
+        x = np.concatenate([base, -base[:-1], [2.0 ** -53, 2.0 ** -60]])
+    else:                # exponents across the whole range: the fallback
+        x = rng.standard_normal(n) * 2.0 ** rng.integers(-1000, 1000, n)
+    got, used = xs(x, "window")
+    assert same(got, math.fsum(x.tolist()))
+    assert (used == -1) if seed % 3 == 2 else (0 < used <= 16)
+    assert xs(np.zeros(3), "window") == (0.0, 0)

@@ -47,6 +47,8 @@ def summarize(d, f):
     for k in ("leads", "pool_push", "pool_take", "give", "cellar_in", "cellar_out", "prefetch", "lock_spins", "spill_records", "chunks_out", "chunks_in",
               "records_out", "records_in", "seed_calls", "mixed_rounds"):
         s[k] = {"sum": col[k].sum(), "max": col[k].max()}
+    polls = d[:, f.index("polls")].astype(np.uint64)
+    s["polls"] = {"sum": float((polls & np.uint64(0xffffffff)).sum()), "saw_ticket": float((polls >> np.uint64(32)).sum())}
     s["t_wait_us_p50"] = float(np.median(col["t_wait"])) / 100.0
     s["max_ring"] = col["max_ring"].max()
     s["seeds"] = {"min": col["seeds"].min(), "max": col["seeds"].max()}
