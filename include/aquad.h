@@ -71,7 +71,10 @@ typedef struct {
     uint64_t tasks;     /* intervals evaluated = Σ tasks_per_process (:162) */
     uint64_t accepted;  /* accepted subintervals (tag-1 area messages, :201) */
     uint32_t levels;    /* 1 + deepest refinement level reached */
-    uint32_t n_cu;      /* CUs that evaluated at least one task (per-CU counts kept: lone-integral launches) */
+    uint32_t n_cu;      /* CUs that evaluated at least one task. Per-CU counts (n_cu, tasks_per_cu) are kept
+                           for the synchronous calls and for launches of fewer than 12 integrals into slots
+                           below 65536; other launches report n_cu = 0 and zero rows (their per-CU work is
+                           still counted by aq_cu_task_counters, which sees every launch) */
     uint64_t spilled;   /* interval pairs moved through the HBM work queue (load balance) */
     uint32_t n_gpus;    /* GPUs that contributed (entries written to tasks_per_gpu) */
     uint32_t reserved;
@@ -89,8 +92,9 @@ void aq_ctx_destroy(aq_ctx *ctx);
 const char *aq_strerror(int code);
 /* Compute units of the context's device (one persistent workgroup each). */
 int aq_ctx_num_cus(const aq_ctx *ctx);
-/* Wavefront workers of the on-device farmer (workgroups x waves per workgroup): one integral
- * launched alone is split into this many shares (the partition aq_integrate_shard documents). */
+/* Wavefront workers of the on-device farmer (workgroups x 12 waves per workgroup): the partition of
+ * sharded and multi-integral launches (aq_integrate_shard documents it). An unsharded lone integral
+ * runs 8 waves per workgroup (its set-up and seeding are issue-bound at three waves per SIMD). */
 int aq_ctx_num_workers(const aq_ctx *ctx);
 /* Device memory the context holds, bytes. */
 int aq_ctx_device_bytes(const aq_ctx *ctx, uint64_t *bytes);

@@ -248,7 +248,7 @@ class Context:
     DIAG_FIELDS = ("t_start", "t_seeded", "t_first_lead", "t_exit", "rounds", "tasks", "chunks_out", "chunks_in",
                    "records_out", "t_wait", "leads", "seeds", "pool_push", "cu", "records_in", "active_lanes",
                    "c_round", "c_eval", "pool_take", "lock_spins", "t_last_round", "spill_records", "max_ring", "c_seed",
-                   "seed_calls", "c_seed_resolve", "mixed_rounds", "c_idle", "c_seed_pass1", "c_seed_pass2", "give", "cellar_in",
+                   "seed_calls", "c_seed_resolve", "max_cellar", "c_idle", "c_seed_pass1", "c_seed_pass2", "give", "cellar_in",
                    "cellar_out", "c_refill", "c_loop", "active_tasks", "prefetch", "t_init", "t_done", "t_fold",
                    "t_broke", "t_flushed", "c_p1_class", "c_p1_walk", "c_p1_f", "t_seed_in", "t_class", "polls")
     DIAG_WORDS = 48

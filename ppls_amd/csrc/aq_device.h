@@ -145,7 +145,7 @@ __device__ __forceinline__ void task_step_k(const double (&l)[K], const double (
 // the widths of :189 / :190 -- the reference's values, one operation each, so the three midpoints
 // cost three adds and one multiply where (l + r) / 2 costs an add and a multiply each. The
 // children pairs are {ha, hm} and {hm, hb}: already at hand. Returns m and hm for the pushes.
-template <int FID>
+template <int FID, unsigned TABMASK = 127u>
 __device__ __forceinline__ void pair_step_halves(double ha, double hb, double fa, double fm, double fb, double eps2,
                                                  const ExpEntry* __restrict__ tab, Step2 (&s)[2], double& m,
                                                  double& hm, const ExpConsts& kk, int range_hint,
@@ -165,7 +165,7 @@ __device__ __forceinline__ void pair_step_halves(double ha, double hb, double fa
 #pragma unroll
     for (int k = 0; k < 2; ++k) asm volatile("" : "+v"(lr2e[k]), "+v"(wl[k]), "+v"(wr[k]));
     double fmid[2];
-    integrand_k<FID, 2, (f_scale<FID>() != 1.0)>(mid, fmid, tab, kk, range_hint, out_mask);   // :188
+    integrand_k<FID, 2, (f_scale<FID>() != 1.0), TABMASK>(mid, fmid, tab, kk, range_hint, out_mask);   // :188
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         s[k].fmid = fmid[k];

@@ -353,7 +353,10 @@ __device__ __forceinline__ bool cosh_main_range(double x) {
 // RN(0.5 / t) = RN(q + r y2) = 0.5 RN(y2 + e y2) = 0.5 y3 (the next Newton iterate), and cosh =
 // RN(0.5 t + 0.5 y3) = 0.5 RN(t + y3): every halving is exact in this range. One multiply fewer per
 // evaluation and a shorter chain (e, y3, t + y3 against q, r, h, c).
-template <int K, bool CHECK = true, bool TWICE = false>
+// TABMASK: 127 for the 128-entry LDS table; 255 for a table of its 128 entries twice over (k_stream's
+// bulk instance, AQ_WIDE_TAB): the index is then ki's low byte, one SDWA shift (no and, no or of the
+// table's base, which the read's offset field carries).
+template <int K, bool CHECK = true, bool TWICE = false, unsigned TABMASK = 127u>
 __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K], const ExpEntry* __restrict__ tab,
                                             const ExpConsts& kk) {
     double ax[K], kd[K], r[K], r2[K], tmp[K], t[K];
@@ -365,7 +368,7 @@ __device__ __forceinline__ bool cosh_main_k(const double (&x)[K], double (&c)[K]
         ax[k] = fabs(x[k]);
         kd[k] = __fma_rn(kk.inv, ax[k], kk.shift);
         ki[k] = (uint64_t)__double_as_longlong(kd[k]);
-        e[k] = tab[ki[k] & 127];
+        e[k] = tab[ki[k] & TABMASK];
         if (CHECK) out |= !cosh_main_range(x[k]);
     }
 #pragma unroll
@@ -427,7 +430,7 @@ __device__ __forceinline__ bool cosh_main_span(double lo, double hi) {
 //
 // SCALED (cosh^4 only): f[k] = 16 F(x[k]), exactly, as ((s*s)*s)*s with s = 2 cosh (cosh_main_k
 // TWICE): every product is the reference's scaled by a power of two (f_scale<FID>(), aq_device.h).
-template <int FID, int K, bool SCALED = false>
+template <int FID, int K, bool SCALED = false, unsigned TABMASK = 127u>
 __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K], const ExpEntry* __restrict__ tab,
                                             const ExpConsts& kk = ExpConsts{}, int range_hint = -1,
                                             unsigned long long out_mask = 0ull) {
@@ -436,7 +439,7 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
         double c[K];
         bool out;
         if (range_hint == 2) {
-            cosh_main_k<K, false, SCALED>(x, c, tab, kk);
+            cosh_main_k<K, false, SCALED, TABMASK>(x, c, tab, kk);
             if (__builtin_expect(out_mask != 0ull, 0)) {
 #pragma unroll
                 for (int k = 0; k < K; ++k)
@@ -444,10 +447,10 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
             }
             out = false;
         } else if (range_hint >= 0) {
-            cosh_main_k<K, false, SCALED>(x, c, tab, kk);
+            cosh_main_k<K, false, SCALED, TABMASK>(x, c, tab, kk);
             out = range_hint == 0;
         } else {
-            out = cosh_main_k<K, true, SCALED>(x, c, tab, kk);
+            out = cosh_main_k<K, true, SCALED, TABMASK>(x, c, tab, kk);
         }
         if (__builtin_expect(__ballot(out) != 0ull, 0)) {
 #pragma unroll

@@ -158,6 +158,9 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 // keeps the 100 MHz realtime clock at a few points of its life in registers and stores them once at
 // its exit (g_aq_stamps, read back by aq_debug_stamps) -- the lone launch's timeline without the DIAG
 // instance's LDS atomics
+#ifndef AQ_WIDE_TAB
+#define AQ_WIDE_TAB 1   // the bulk cosh4 instance's 256-entry exp table (k_stream WIDE)
+#endif
 #ifndef AQ_STAMPS
 #define AQ_STAMPS 0
 #endif
@@ -429,7 +432,7 @@ enum : int {
     DG_T_START = 0, DG_T_SEEDED, DG_T_FIRST_LEAD, DG_T_EXIT, DG_ROUNDS, DG_TASKS, DG_CHUNKS_OUT, DG_CHUNKS_IN,
     DG_RECORDS_OUT, DG_T_WAIT, DG_LEADS, DG_SEEDS, DG_POOL_PUSH, DG_CU, DG_RECORDS_IN, DG_ACTIVE_LANES,
     DG_C_ROUND, DG_C_EVAL, DG_POOL_TAKE, DG_LOCK_SPINS, DG_T_LAST_ROUND, DG_SPILL_RECORDS, DG_MAX_RING, DG_C_SEED,
-    DG_SEED_CALLS, DG_FLUSHES, DG_MIXED_ROUNDS, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_CELLAR_IN,
+    DG_SEED_CALLS, DG_FLUSHES, DG_MAX_CELLAR, DG_C_IDLE, DG_C_LOCK, DG_C_SHARE, DG_GIVE, DG_CELLAR_IN,
     DG_CELLAR_OUT, DG_C_REFILL, DG_C_LOOP, DG_ACTIVE_TASKS, DG_PREFETCH, DG_T_INIT, DG_T_DONE, DG_T_FOLD,
     DG_T_BROKE, DG_T_FLUSHED, DG_C_P1_CLASS, DG_C_P1_WALK, DG_C_P1_F, DG_T_SEED_IN, DG_T_CLASS, DG_POLLS,
     DIAG_WORDS = 48
@@ -689,14 +692,24 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
     // pair stores no midpoint: m = (a + b) / 2 is recomputed with the parent's own operands (:187),
     // bit-identical, so a pair is 44 B and a ring holds 256 pairs.
-    __shared__ double s_pr[6 * LREC];
+    // The integrand table first: it must lie in the LDS's first 64 KiB for the round's table reads to
+    // carry its base in their offset field (WIDE). WIDE: the bulk cosh4 instance keeps exp's 128
+    // entries twice over, indexed by ki's low byte (cosh_main_k TABMASK; the per-CU instance's LDS has
+    // no 2 KiB to spare beside its per-integral accumulators)
+    constexpr bool WIDE = AQ_WIDE_TAB && FID == F_COSH4 && !PCU;
+    // (the compiler places the largest LDS object first: the wide table shares the pair block's array, at
+    // its front -- offset 0 -- and the pairs start 4 KiB in, a multiple of a ring's 2 KiB per field)
+    constexpr int TAB_FRONT = WIDE ? 256 * 16 / 8 : 0;   // doubles ahead of the pair block
+    __shared__ double s_lds[TAB_FRONT + 6 * LREC];
+    double* const s_pr = s_lds + TAB_FRONT;
+    __shared__ ExpEntry tab_own[WIDE ? 1 : ftab_entries<FID>()];   // exp's, or sin(1/x)'s __sincostab (stage_f_table)
+    ExpEntry* const tab = WIDE ? reinterpret_cast<ExpEntry*>(s_lds) : tab_own;
     const DtField s_dt{reinterpret_cast<unsigned*>(s_pr + 5 * LREC)};
     double* const s_a = s_pr;
     double* const s_b = s_pr + LREC;
     double* const s_fa = s_pr + 2 * LREC;
     double* const s_fm = s_pr + 3 * LREC;
     double* const s_fb = s_pr + 4 * LREC;
-    __shared__ ExpEntry tab[ftab_entries<FID>()];   // exp's, or sin(1/x)'s __sincostab (stage_f_table)
     __shared__ WgState S;
     __shared__ unsigned long long s_pc[PCU ? 3 * PCU_ROW : 1];
     __shared__ XSum s_px[PCU ? PCU_ROW : 1];
@@ -727,7 +740,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     // round reads ring slots only through masked pops of pushed pairs -- the fill's 18 K LDS stores per
     // CU had cost every launch 0.75 us, r04j)
     ExpPair tv{};
-    if (FID != F_SIN_RECIP && tid < 128u) tv = reinterpret_cast<const ExpPair*>(kExpTabBits)[tid];
+    if (FID != F_SIN_RECIP && tid < (WIDE ? 256u : 128u)) tv = reinterpret_cast<const ExpPair*>(kExpTabBits)[tid & 127u];
     static_assert(FID != F_SIN_RECIP || AQ_SINCOS_TAB_N <= PTT, "one sin-table entry per thread");
     double sv = 0.0;
     if (FID == F_SIN_RECIP && tid < (unsigned)AQ_SINCOS_TAB_N) sv = kSinCosTab[tid];
@@ -746,7 +759,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     }
     if (FID == F_SIN_RECIP) {
         if (tid < (unsigned)AQ_SINCOS_TAB_N) reinterpret_cast<double*>(tab)[tid] = sv;
-    } else if (tid < 128u) {
+    } else if (tid < (WIDE ? 256u : 128u)) {
         tab[tid].tail_bits = tv.tail_bits;
         tab[tid].sbits = tv.sbits;
     }
@@ -848,7 +861,12 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             lds_wait6(r);
             chunk_store(&cel->c[(c + q) / 64u], lane, r);
         }
-        if constexpr (DIAG) { if (lane == 0) atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL); }
+        if constexpr (DIAG) {
+            if (lane == 0) {
+                atomicAdd(&s_dg[DG_CELLAR_OUT], (unsigned long long)SPILL);
+                atomicMax(&s_dg[DG_MAX_CELLAR], (unsigned long long)(c + SPILL));   // the deepest cellar of the workgroup
+            }
+        }
     };
     const ExpConsts kk = pinned_exp_consts();
     // the depth cap per burst (see the file's configuration notes); the histogram instance keeps the
@@ -1706,7 +1724,8 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             unsigned long long nospan = 0ull;
             if constexpr (FID == F_COSH4) nospan = __ballot((int)dt >= 0);
             double pm, hm;
-            pair_step_halves<FID>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk, FID == F_COSH4 ? 2 : -1, nospan & am);
+            pair_step_halves<FID, WIDE ? 255u : 127u>(pa, pb, pfa, pfm, pfb, eps2, tab, st, pm, hm, kk,
+                                                       FID == F_COSH4 ? 2 : -1, nospan & am);
             if constexpr (prio_by_load) { if (!b_heavy) asm volatile("s_setprio 0"); }
             const unsigned long long r0m = __ballot(st[0].refine), r1m = __ballot(st[1].refine);
             unsigned long long okm = am;
@@ -1719,8 +1738,10 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             const unsigned long long l0m = am & ~r0m, l1m = am & ~r1m;
             b_n += na;   // tasks 2 na; accepted: once per burst from the growth of S (below)
             const unsigned long long mask0 = okm & r0m, mask1 = okm & r1m;
-            const unsigned long long cdtw = dtw + 1ull;   // depth + 1, same integral
-            const unsigned cdt = (unsigned)cdtw;
+            // depth + 1, same integral: a 32-bit add on the word's low half (the depth byte never carries
+            // past bit 7, static_assert above); the high half of the 8-byte field is carried unread
+            const unsigned cdt = dt + 1u;
+            const unsigned long long cdtw = ((dtw >> 32) << 32) | (unsigned long long)cdt;
             masked_acc3(acc.r, st[0].area2, l0m, st[1].area2, l1m, acc.maxdt, burst_cap ? cdt : dt,
                         burst_cap ? (mask0 | mask1) : am);
             if constexpr (DIAG) {
@@ -1807,6 +1828,9 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             __builtin_amdgcn_wave_barrier();
             if (!b_go) break;
         }
+        // (a heavy burst ran at priority 3: back to 0 before the push-back, the outer loop, the locks and
+        // the leader's polls -- ADVICE r4)
+        if constexpr (prio_by_load) asm volatile("s_setprio 0");
         // the held pairs back on top of the ring
         lds_push6_masked(b_am, ring_addr(ring8, ring_slot(b_top) + mbcnt(b_am), ring_vmask), ca, cb, cfa, cfm, cfb,
                          cdw);

@@ -320,6 +320,32 @@ def test_cu_task_counters_every_launch(ctx, trees):
         ctx.set_level_histograms(True)
 
 
+def test_small_launches_in_high_slots(ctx, trees):
+    """launches of fewer than 12 integrals run the per-CU instance only while their
+    slots lie below 65536 (the per-workgroup words exist for those); at first_slot 65531 with 11
+    integrals (straddling the boundary), 200000 and the last slot, they run the bulk instance with a
+    static job stride. Counts exact and areas within 1e-12 everywhere; the per-CU row is kept below
+    65536 and documented as absent above (n_cu = 0, include/aquad.h) -- the context's per-CU counters
+    (aq_cu_task_counters) count every launch either way."""
+    g = trees["cosh4_eps1e-8"]
+    ctx.set_level_histograms(False)
+    try:
+        for first, k in [(65531, 1), (65531, 11), (200000, 1), (200000, 11), (ctx.async_slots - 1, 1)]:
+            ctx.cu_task_counters(reset=True)
+            ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-8, first_slot=first)
+            for i in range(k):
+                r = ctx.fetch(first + i, detail=True)
+                assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"]), (first, k, i)
+                assert _area_ok(r.area, g["area_quad"]), (first, k, i)
+                if first + k <= 65536:
+                    assert r.n_cu >= 1 and sum(r.tasks_per_cu.values()) == r.tasks
+                else:
+                    assert r.n_cu == 0 and r.tasks_per_cu == {}
+            assert sum(ctx.cu_task_counters(reset=True).values()) == k * g["tasks"]
+    finally:
+        ctx.set_level_histograms(True)
+
+
 def _gather(ctx, n):
     """Rows {area, tasks, accepted, error} of slots 0..n-1 (aq_gather_results into a device buffer)."""
     import torch

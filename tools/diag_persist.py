@@ -45,7 +45,7 @@ def summarize(d, f):
     s["tasks"] = {"min": col["tasks"].min(), "p50": float(np.median(col["tasks"])), "max": col["tasks"].max(),
                   "sum": col["tasks"].sum()}
     for k in ("leads", "pool_push", "pool_take", "give", "cellar_in", "cellar_out", "prefetch", "lock_spins", "spill_records", "chunks_out", "chunks_in",
-              "records_out", "records_in", "seed_calls", "mixed_rounds"):
+              "records_out", "records_in", "seed_calls", "max_cellar"):
         s[k] = {"sum": col[k].sum(), "max": col[k].max()}
     polls = d[:, f.index("polls")].astype(np.uint64)
     s["polls"] = {"sum": float((polls & np.uint64(0xffffffff)).sum()), "saw_ticket": float((polls >> np.uint64(32)).sum())}

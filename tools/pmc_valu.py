@@ -30,7 +30,7 @@ FP64_PEAK = 78.6e12
 FLOP_PER_TASK = 38
 WAVES_PER_SIMD = 3
 N_SIMD = 1024
-KERNEL = "k_stream<0, false, false, false>"
+KERNEL = "k_stream<0, false, false, false"   # (r05: a fifth template argument, the waves per workgroup)
 
 
 def counters(path):
