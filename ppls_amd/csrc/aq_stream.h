@@ -216,7 +216,13 @@ constexpr int DEFAULT_GSPLIT = AQ_GSPLIT_DEFAULT;  // a multi-integral launch's 
 #define AQ_TASKS_PER_JOB 120000
 #endif
 constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a job holds about this many tasks
-constexpr int CCAP = 4096;          // pairs per wave cellar (private HBM overflow stack, 208 KiB)
+#ifndef AQ_CCAP
+#define AQ_CCAP 2048
+#endif
+// pairs per wave cellar (private HBM overflow stack, 96 KiB). The deepest cellar of any wave measured
+// 448 pairs at eps=1e-10 and 576 at 1e-12 (DIAG max_cellar, every workgroup, profiles/r05o); 4096 had
+// held 604 MB per context for nothing. A wave whose cellar is full spills to the pool / HBM queue.
+constexpr int CCAP = AQ_CCAP;
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 #ifndef AQ_PF_BELOW
 // r02 A/B (8192-integral launch, GIVE_ROUNDS 32): 112 28.39, 96 27.93, 80 27.57, 64 27.20, 48 28.18,

@@ -623,13 +623,14 @@ def test_plugin_reference_printout(ctx, trees):
 
 
 def test_context_footprint():
-    """No per-wave area partials or second engine: a fresh context holds ~1.6 GiB -- 262144 result
-    slots (738 MB, r04: 8 x 32768 per launch), the wave cellars (604 MB), the per-CU words of the
-    first 65536 slots (268 MB) and the HBM queue -- of the GPU's 288 GB (round 1: ~7 GiB; the level
-    path's two 512 MiB frontiers are allocated only when aq_integrate_levels first runs)."""
+    """No per-wave area partials or second engine: a fresh context holds ~1.3 GiB -- 262144 result
+    slots (738 MB, r04: 8 x 32768 per launch), the wave cellars (302 MB: 2048 pairs each since r05,
+    from 4096), the per-CU words of the first 65536 slots (268 MB) and the HBM queue -- of the GPU's
+    288 GB (round 1: ~7 GiB; the level path's two 512 MiB frontiers are allocated only when
+    aq_integrate_levels first runs)."""
     from ppls_amd import Context
     with Context(0) as c:
-        assert c.device_bytes < 1.75 * 2 ** 30, c.device_bytes
+        assert c.device_bytes < 1.45 * 2 ** 30, c.device_bytes
 
 
 def test_exact_rows_sum_over_shards(ctx, trees):
