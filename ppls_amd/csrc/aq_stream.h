@@ -1084,6 +1084,8 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 // once per job. A scalar load (lgkmcnt), so the wait for it does not also wait for the
                 // previous integral's flush atomics and this job's claim (vmcnt, in issue order), which
                 // stay in flight while the job seeds (C3 eps=1e-3 A/B: profiles/r02_ab/sload_bounds.txt)
+                // (a select between kbounds[0] and kbounds[p] put the whole 400-B argument block in
+                // scratch: lone launches +10 us, profiles/r05r)
                 const double2 ab = PCU ? P.kbounds[p] : sload_bounds(P.bounds, p);
                 if (static_jobs) {
                     // launches of few integrals cut every integral into one share per wave: wave w seeds share w of

@@ -25,7 +25,8 @@ NAMES = ["entry", "init", "seed_in", "seeded", "idle", "lead", "broke", "flushed
          "pre", "class", "feval", "done", "karg"]
 ORDER = ["entry", "karg", "pre", "init", "seed_in", "class", "feval", "seeded", "idle", "lead", "done", "broke",
          "flushed", "exit"]
-ST_XCC, ST_STRIDE, NW = 9, 16, 12
+ST_XCC, ST_STRIDE = 9, 16
+NW = int(os.environ.get("AQ_STAMPS_NW", "8"))   # waves per workgroup of the lone instance (aq_abi.inc AQ_LONE_NW)
 
 
 def timeline(ctx, grid):
