@@ -29,7 +29,7 @@ def summarize(d, f):
     s["cyc_per_round"] = float(np.median(col["c_round"] / r))
     s["cyc_eval_per_round"] = float(np.median(col["c_eval"] / r))
     s["cyc_seed_per_call"] = float(col["c_seed"].sum() / max(col["seed_calls"].sum(), 1))
-    for k in ("c_seed_pass1", "c_seed_pass2", "c_seed_resolve"):
+    for k in ("c_seed_pass1", "c_seed_pass2", "c_seed_resolve", "c_p1_class", "c_p1_walk", "c_p1_f"):
         s["cyc_" + k[2:] + "_per_call"] = float(col[k].sum() / max(col["seed_calls"].sum(), 1))
     s["cyc_idle_per_wg_p50"] = float(np.median(col["c_idle"]))
     s["cyc_round_per_wg_p50"] = float(np.median(col["c_round"]))
