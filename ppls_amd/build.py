@@ -36,7 +36,7 @@ USER_F = os.path.abspath(os.environ.get("PPLS_AMD_USER_F") or os.path.join(CSRC,
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("aq_libm.h", "aq_exp_table.h", "aq_sincos_table.h", "aq_device.h", "aq_stream.h",
                                                   "aq_xsum.h", "aq_abi.inc")] + \
     [os.path.join(ROOT, "include", "aquad.h"), USER_F]
-LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+LIBS = ["-pthread", "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _stale(target, deps):

@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "aquad.h"
@@ -147,13 +148,16 @@ __global__ __launch_bounds__(256) void k_batch_estimate(const double2* __restric
 }
 
 // Scatter the chunk into size order: sorted[pos] = bounds[i], perm[pos] = i, pos = the key's offset (an
-// exclusive scan of counts) + this block's reserved range + the thread's rank within it.
+// exclusive scan of counts) + this block's reserved range + the thread's rank within it. Block 0 also
+// zeroes `next` (the other chunk parity's counts and cursors, 2 EST_KEYS words: the next chunk's
+// estimate adds into them; the previous chunk's scatter is done with them).
 __global__ __launch_bounds__(256) void k_batch_scatter(const double2* __restrict__ bounds, const unsigned* __restrict__ key_of,
                                                        int n, const unsigned* __restrict__ counts,
                                                        unsigned* __restrict__ cursor, double2* __restrict__ sorted,
-                                                       unsigned* __restrict__ perm) {
+                                                       unsigned* __restrict__ perm, unsigned* __restrict__ next) {
     __shared__ unsigned s_off[EST_KEYS], s_cnt[EST_KEYS], s_base[EST_KEYS];
     const unsigned t = threadIdx.x;
+    if (blockIdx.x == 0 && t < 2u * EST_KEYS) next[t] = 0u;
     if (t < EST_KEYS) {
         s_cnt[t] = 0u;
         if (t == 0) {

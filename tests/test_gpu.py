@@ -582,6 +582,28 @@ def test_c3_eps1e10_max_launch(ctx, oracle, batch_golden):
         assert abs(rows[i, 0] - oa[j]) <= AREA_RTOL * abs(oa[j])
 
 
+def test_fresh_context_first_tiny_batch(oracle, batch_golden):
+    """A fresh context's first launch of many tiny trees (C3 at eps=1e-3, 65536 integrals) takes ~16 W
+    jobs in all, not 16 per integral: with ~90-task jobs it had been seeding-bound (13 ms where a
+    sized launch takes ~0.5, profiles/r05w). Counts exact, and the kernel well under that."""
+    from ppls_amd import Context
+    k = 65536
+    a, b = oracle.batch_bounds(k)
+    with Context(0) as c:
+        c.set_level_histograms(False)
+        c.kernel_timing(True)
+        area, tasks, acc = c.integrate_batch(a, b, 1e-3)
+        ms, n = c.kernel_time()
+        c.kernel_timing(False)
+    assert (tasks == 2 * acc - 1).all()
+    first = batch_golden["leaves_eps1e-3_first256"]
+    assert [int(v) for v in acc[:len(first)]] == first
+    kn = batch_golden["n_eps1e-3"]
+    assert int(acc[:kn].sum()) == batch_golden["sum_leaves_eps1e-3"]
+    assert int(tasks[:kn].sum()) == batch_golden["sum_tasks_eps1e-3"]
+    assert ms < 4.0, ms
+
+
 def test_stall_bound_is_not_a_run_time_cap(ctx, deep_golden):
     """A launch far longer than the stall bound (50 ms here; 1024 integrals at eps=1e-16, 1.5e11
     tasks) completes with exact counts: the on-device wait is bounded by time without progress only."""

@@ -65,18 +65,23 @@ def main():
     args = ap.parse_args()
     ctx = Context(0)
     ctx.set_level_histograms(False)
+    if args.c3:
+        from tools.bench_batch import splitmix64_bounds
+        a, b = splitmix64_bounds(args.k)
+    else:
+        a, b = np.zeros(args.k), np.full(args.k, 5.0)
+    if args.k > 1:
+        # one plain launch of the same workload first: its tasks size the DIAG launch's jobs, as in the
+        # bench (a fresh context's first launch runs the default job split)
+        ctx.integrate_many_async(a, b, args.eps)
+        ctx.fetch(args.k - 1)
     ctx.set_diagnostics(True)
     res = []
     for _ in range(args.reps):
         if args.k == 1:
             r = ctx.integrate(Problem(eps=args.eps))
         else:
-            if args.c3:
-                from tools.bench_batch import splitmix64_bounds
-                a, b = splitmix64_bounds(args.k)
-                ctx.integrate_many_async(a, b, args.eps)
-            else:
-                ctx.integrate_many_async(np.zeros(args.k), np.full(args.k, 5.0), args.eps)
+            ctx.integrate_many_async(a, b, args.eps)
             r = ctx.fetch(args.k - 1)
         d, f = ctx.diagnostics()
         res.append(summarize(d, f))
