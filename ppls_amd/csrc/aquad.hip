@@ -97,15 +97,21 @@ __global__ __launch_bounds__(256) void k_eval(const double* __restrict__ x, doub
 // uses it: the counts and areas of every integral are those of its own tree whatever the order.
 // ------------------------------------------------------------------------------------------------
 constexpr int EST_KEYS = 64;   // size classes: key 0 = largest (descending 6 log2(1 + est))
+// tasks per unit of the estimate: 2.77-2.90 over cosh4 [0,5] at eps = 1e-3 ... 1e-12 and 2.84 for C3's
+// mean at 1e-3 and 1e-10 (an offline check with the host integrand), so a fresh workload's first launch
+// can size its jobs from it (k_batch_scatter)
+constexpr double EST_TASKS = 2.84;
 template <int FID>
 __global__ __launch_bounds__(256) void k_batch_estimate(const double2* __restrict__ bounds, int n, double eps,
                                                         unsigned* __restrict__ key_of, unsigned* __restrict__ counts,
-                                                        const ExpPair* __restrict__ gtab) {
+                                                        double* __restrict__ est_sum, const ExpPair* __restrict__ gtab) {
     __shared__ ExpEntry tab[ftab_entries<FID>()];
     __shared__ unsigned s_cnt[EST_KEYS];
+    __shared__ double s_est[4];
     stage_f_table<FID>(tab, gtab);
     if (threadIdx.x < EST_KEYS) s_cnt[threadIdx.x] = 0u;
     __syncthreads();
+    double est = 0.0;
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i < n) {
         const double2 ab = bounds[i];
@@ -119,7 +125,6 @@ __global__ __launch_bounds__(256) void k_batch_estimate(const double2* __restric
 #pragma unroll
         for (int k = 0; k < 17; ++k) f[k] = integrand<FID>(x[k], tab);   // :188
         bool alive[16] = {true};
-        double est = 0.0;
 #pragma unroll
         for (int d = 0, s = 16; d < 4; ++d, s >>= 1) {
 #pragma unroll
@@ -143,21 +148,40 @@ __global__ __launch_bounds__(256) void k_batch_estimate(const double2* __restric
         key_of[i] = key;
         atomicAdd(&s_cnt[key], 1u);
     }
+    // the block's sum of the estimates (one atomic per block)
+    for (int o = 32; o >= 1; o >>= 1) est += __shfl_xor(est, o, 64);
+    if ((threadIdx.x & 63u) == 0u) s_est[threadIdx.x >> 6] = est;
     __syncthreads();
     if (threadIdx.x < EST_KEYS && s_cnt[threadIdx.x]) atomicAdd(&counts[threadIdx.x], s_cnt[threadIdx.x]);
+    if (threadIdx.x == 0) atomicAdd(est_sum, (s_est[0] + s_est[1]) + (s_est[2] + s_est[3]));
 }
 
 // Scatter the chunk into size order: sorted[pos] = bounds[i], perm[pos] = i, pos = the key's offset (an
 // exclusive scan of counts) + this block's reserved range + the thread's rank within it. Block 0 also
-// zeroes `next` (the other chunk parity's counts and cursors, 2 EST_KEYS words: the next chunk's
-// estimate adds into them; the previous chunk's scatter is done with them).
+// zeroes `next` / `next_est` (the other chunk parity's counts, cursors and estimate sum: the next
+// chunk's estimate adds into them; the previous chunk's scatter is done with them) and, for a fresh
+// workload (hint != null), sets the launch's job size from the chunk's mean estimate: shares per
+// integral for ~TASKS_PER_JOB tasks per job, as the end of an adaptive launch does from its measured
+// tasks (a first launch of tiny trees with the default 16 shares had been seeding-bound, profiles/r05w).
 __global__ __launch_bounds__(256) void k_batch_scatter(const double2* __restrict__ bounds, const unsigned* __restrict__ key_of,
                                                        int n, const unsigned* __restrict__ counts,
                                                        unsigned* __restrict__ cursor, double2* __restrict__ sorted,
-                                                       unsigned* __restrict__ perm, unsigned* __restrict__ next) {
+                                                       unsigned* __restrict__ perm, unsigned* __restrict__ next,
+                                                       const double* __restrict__ est_sum, double* __restrict__ next_est,
+                                                       LaunchHint* __restrict__ hint, unsigned max_shares) {
     __shared__ unsigned s_off[EST_KEYS], s_cnt[EST_KEYS], s_base[EST_KEYS];
     const unsigned t = threadIdx.x;
-    if (blockIdx.x == 0 && t < 2u * EST_KEYS) next[t] = 0u;
+    if (blockIdx.x == 0) {
+        if (t < 2u * EST_KEYS) next[t] = 0u;
+        if (t == 0) {
+            *next_est = 0.0;
+            if (hint) {
+                const double per = EST_TASKS * *est_sum / (double)max(n, 1);   // predicted tasks per integral
+                const double sh = floor((per + 0.5 * TASKS_PER_JOB) / TASKS_PER_JOB);
+                hint->shares_next = (unsigned)fmin(fmax(sh, 1.0), (double)max_shares);
+            }
+        }
+    }
     if (t < EST_KEYS) {
         s_cnt[t] = 0u;
         if (t == 0) {

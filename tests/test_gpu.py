@@ -583,9 +583,10 @@ def test_c3_eps1e10_max_launch(ctx, oracle, batch_golden):
 
 
 def test_fresh_context_first_tiny_batch(oracle, batch_golden):
-    """A fresh context's first launch of many tiny trees (C3 at eps=1e-3, 65536 integrals) takes ~16 W
-    jobs in all, not 16 per integral: with ~90-task jobs it had been seeding-bound (13 ms where a
-    sized launch takes ~0.5, profiles/r05w). Counts exact, and the kernel well under that."""
+    """A fresh context's first batch of tiny trees (C3 at eps=1e-3, 65536 integrals): the size
+    pre-pass sets the first launch's job size (whole-integral jobs here) instead of the default 16
+    shares per integral, with which ~90-task jobs had made it seeding-bound (13 ms where a sized launch
+    takes ~0.5, profiles/r05w). Counts exact, and the kernel well under that."""
     from ppls_amd import Context
     k = 65536
     a, b = oracle.batch_bounds(k)

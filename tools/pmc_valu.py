@@ -1,7 +1,7 @@
 """Fold rocprofv3 --pmc passes of the bench launch (tools/pmc_bench_launch.py under tools/r05_pmc_valu.sh)
 into the FP64 / VALU figures the roofline line carries (profiles/<tag>/pmc_valu.json). Diagnostic tool.
 
-  python tools/pmc_valu.py <dir> [--tasks T] [--round-valu 98] [--tasks-per-round 127.17] > pmc_valu.json
+  python tools/pmc_valu.py <dir> [--tasks T] [--round-valu 96] [--tasks-per-round 127.17] > pmc_valu.json
 
 <dir> holds p*/run_counter_collection.csv (one rocprofv3 --pmc pass each) and kt/run_kernel_trace.csv
 (the kernel-trace pass of the same command). Only the k_stream dispatches of the bench shape count (the
@@ -56,7 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--tasks", type=float, default=32768 * 1464273.0, help="tasks per dispatch")
-    ap.add_argument("--round-valu", type=float, default=98.0)
+    ap.add_argument("--round-valu", type=float, default=96.0)
     ap.add_argument("--tasks-per-round", type=float, default=None)
     ap.add_argument("--tag", default=None, help="profiles/<tag> the summary is committed under")
     a = ap.parse_args()
