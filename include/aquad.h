@@ -248,7 +248,11 @@ int aq_cu_task_counters(aq_ctx *ctx, uint64_t *out, int cap, int reset);
  * against another order compiles and gets the arrays swapped). The integrals run in launches of up
  * to aq_max_integrals_per_launch(); each launch's bounds are validated just before it is enqueued,
  * so a bad bound in a later launch returns AQ_EINVAL after the earlier launches ran: the outputs
- * are then unspecified (not all-or-nothing). */
+ * are then unspecified (not all-or-nothing). Each launch runs its integrals largest-first (a device
+ * pre-pass estimates every tree's size; only the order changes, never a result); the host checks,
+ * stages and unpacks on up to 8 threads. Environment: AQ_BATCH_SORT=0 keeps the input order,
+ * AQ_HOST_THREADS=<n> bounds the host threads, AQ_BATCH_FIRST / AQ_BATCH_LAST set the first / last
+ * launch's size (defaults 131072 / no split). */
 int aq_integrate_batch(aq_ctx *ctx, size_t n, const double *a, const double *b, double eps, int integrand,
                        double *area, uint64_t *accepted, uint64_t *tasks);
 
