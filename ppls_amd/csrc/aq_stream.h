@@ -173,8 +173,11 @@ constexpr unsigned LAZY_TICKET = 64;
 // at 1 and drop to 0 after their F chains -- the waves holding the most work win the SIMD's issue
 // (config-4 lone 80.6 -> 76.8 us; for cosh4 no gain at thresholds 32 / 64 / 128, r04p)
 constexpr unsigned HEAVY_S = 64;
+// (ST_CB .. ST_NR are sums, not stamps: shader cycles inside bursts and in the wave's loop, bursts
+// and rounds -- where a long launch's wave time goes, tools/stamps_burst.py)
 enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
-             ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_N, ST_STRIDE = 16 };
+             ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_CB, ST_CL, ST_NB, ST_NR, ST_N,
+             ST_STRIDE = 20 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from one integral to the next
@@ -858,6 +861,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
         if (tid == 0) s_dg[DG_T_START] = t_entry;
         cl0 = clk();
     }
+    if constexpr (AQ_STAMPS && !DIAG) cl0 = clk();
 
     // the ring's bottom SPILL pairs (ring index b) to the cellar's chunks from pair c (whole chunks)
     auto spill_to_cellar = [&](unsigned b, unsigned c) {
@@ -1672,6 +1676,8 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
         // the burst's state, re-asserted uniform (readfirstlane) once per burst: the outer loop's many
         // paths leave the compiler unsure, and a "divergent" ring index turns every round's index
         // arithmetic and the loop exit into VALU / exec-mask work
+        unsigned long long cb0 = 0;
+        if constexpr (AQ_STAMPS && !DIAG) cb0 = clk();
         unsigned b_top = uni(top), b_size = uni(size), b_poll = uni(poll_ctr);
         unsigned b_n = 0;                 // pairs evaluated in this burst (2 tasks each)
         unsigned long long b_dv = 0;      // lanes that met the depth cap with a refining task
@@ -1869,6 +1875,11 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             }
         }
         mixed = b_mixed;
+        if constexpr (AQ_STAMPS && !DIAG) {
+            stp[ST_CB] += clk() - cb0;
+            stp[ST_NB] += 1ull;
+            stp[ST_NR] += (unsigned long long)(b_max - b_rem);
+        }
         __builtin_amdgcn_wave_barrier();   // reconverge before the loop latch (keeps wave state uniform)
     }
 
@@ -1960,6 +1971,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
 #if AQ_STAMPS
     if constexpr (!DIAG) {
         stamp(ST_EXIT);
+        stp[ST_CL] = clk() - cl0;
         stp[ST_XCC] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
         if (lane < (unsigned)ST_N) {   // vector stores, one word per lane
             unsigned long long v = 0;
