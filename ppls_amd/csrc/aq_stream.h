@@ -175,9 +175,11 @@ constexpr unsigned LAZY_TICKET = 64;
 constexpr unsigned HEAVY_S = 64;
 // (ST_CB .. ST_NR are sums, not stamps: shader cycles inside bursts and in the wave's loop, bursts
 // and rounds -- where a long launch's wave time goes, tools/stamps_burst.py)
+// (ST_CS: cycles in seeding passes, ST_CF: in their flushes of the previous integral, ST_CBD: in their
+// bounds loads, ST_NS: seeding passes)
 enum : int { ST_ENTRY = 0, ST_INIT, ST_SEED_IN, ST_SEEDED, ST_IDLE, ST_LEAD, ST_BROKE, ST_FLUSHED, ST_EXIT,
-             ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_CB, ST_CL, ST_NB, ST_NR, ST_N,
-             ST_STRIDE = 20 };
+             ST_XCC, ST_PRE, ST_CLASS, ST_FEVAL, ST_DONE, ST_KARG, ST_CB, ST_CL, ST_NB, ST_NR, ST_CS, ST_CF,
+             ST_CBD, ST_NS, ST_N, ST_STRIDE = 24 };
 constexpr int READY_STRIDE = 32;    // one ready flag per 128-B line: pollers never share a line
 constexpr int MAXG = 2048;          // max persistent workgroups per launch
 constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from one integral to the next
@@ -1041,6 +1043,8 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 // ---- wave-local seeding of job `job` (see the file header)
                 unsigned long long cs = 0;
                 stamp(ST_SEED_IN);
+                unsigned long long cs_st = 0;
+                if constexpr (AQ_STAMPS && !DIAG) cs_st = clk();
                 if constexpr (DIAG) {
                     cs = clk();
                     if (lane == 0) atomicMax(&s_dg[DG_T_SEED_IN], rtc());
@@ -1079,9 +1083,16 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                     for (unsigned d = 0; d < nlev; ++d) col0 |= 1ull << (d * nb);
                     colmask = uni(col0) << (lane - div_small(lane, nb, nb_rcp) * nb);
                 }
+                unsigned long long cf0 = 0;
+                if constexpr (AQ_STAMPS && !DIAG) cf0 = clk();
                 if (p != tag) {
                     flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
                     tag = p;
+                }
+                if constexpr (AQ_STAMPS && !DIAG) {
+                    const unsigned long long cf1 = clk();
+                    stp[ST_CF] += cf1 - cf0;
+                    cf0 = cf1;
                 }
                 // the bounds load goes out before the claim: waiting for it then leaves the claim (one
                 // contended atomic, not needed before the next job) in flight
@@ -1091,6 +1102,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 // (a select between kbounds[0] and kbounds[p] put the whole 400-B argument block in
                 // scratch: lone launches +10 us, profiles/r05r)
                 const double2 ab = PCU ? P.kbounds[p] : sload_bounds(P.bounds, p);
+                if constexpr (AQ_STAMPS && !DIAG) stp[ST_CBD] += clk() - cf0;
                 if (static_jobs) {
                     // launches of few integrals cut every integral into one share per wave: wave w seeds share w of
                     // each integral in turn (static stride, no claim). 3072 waves claiming through one
@@ -1391,6 +1403,10 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 bot = 0;
                 top = n_seeds;
                 stamp(ST_SEEDED);
+                if constexpr (AQ_STAMPS && !DIAG) {
+                    stp[ST_CS] += clk() - cs_st;
+                    stp[ST_NS] += 1ull;
+                }
                 if constexpr (DIAG) {
                     if (lane == 0) {
                         atomicAdd(&s_dg[DG_SEED_CALLS], 1ull);

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from ppls_amd import Context  # noqa: E402
 
-ST_CB, ST_CL, ST_NB, ST_NR, ST_STRIDE = 15, 16, 17, 18, 20
+ST_CB, ST_CL, ST_NB, ST_NR, ST_CS, ST_CF, ST_CBD, ST_NS, ST_STRIDE = 15, 16, 17, 18, 19, 20, 21, 22, 24
 NW = 12
 
 
@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--k", type=int, default=32768)
     ap.add_argument("--eps", type=float, default=1e-10)
     ap.add_argument("--c3", action="store_true", help="splitmix64 bounds (SURVEY C3) instead of [0, 5]")
+    ap.add_argument("--batch", action="store_true",
+                    help="through aq_integrate_batch (size-ordered chunks; the stamps are its last launch's)")
     args = ap.parse_args()
     ctx = Context(0)
     ctx.set_level_histograms(False)
@@ -38,11 +40,17 @@ def main():
         a, b = splitmix64_bounds(args.k)
     else:
         a, b = np.zeros(args.k), np.full(args.k, 5.0)
-    ctx.integrate_many_async(a, b, args.eps)
-    ctx.fetch(args.k - 1)
-    ctx.kernel_timing(True)
-    ctx.integrate_many_async(a, b, args.eps)
-    r = ctx.fetch(args.k - 1)
+    if args.batch:
+        ctx.integrate_batch(a, b, args.eps)
+        ctx.kernel_timing(True)
+        _, tasks, _ = ctx.integrate_batch(a, b, args.eps)
+        r = type("R", (), {"tasks": int(tasks[-1])})
+    else:
+        ctx.integrate_many_async(a, b, args.eps)
+        ctx.fetch(args.k - 1)
+        ctx.kernel_timing(True)
+        ctx.integrate_many_async(a, b, args.eps)
+        r = ctx.fetch(args.k - 1)
     ms, _ = ctx.kernel_time()
     grid = ctx.num_workers // NW
     n = grid * NW * ST_STRIDE
@@ -60,6 +68,20 @@ def main():
            "rounds_per_burst": float(nr.sum() / max(nb.sum(), 1.0)),
            "bursts": float(nb.sum()), "rounds": float(nr.sum()),
            "loop_cycles_per_wave_q": q(cl)}
+    ns = max(s[:, ST_NS].sum(), 1.0)
+    out["seeding"] = {"passes": float(ns), "share_of_loop": float(s[:, ST_CS].sum() / cl.sum()),
+                      "cycles_per_pass": float(s[:, ST_CS].sum() / ns),
+                      "flush_cycles_per_pass": float(s[:, ST_CF].sum() / ns),
+                      "bounds_cycles_per_pass": float(s[:, ST_CBD].sum() / ns)}
+    # the launch's timeline: quantiles over waves of the realtime stamps (us after the first entry) --
+    # first seeding, first idle (out of jobs), first lead, end seen, exit
+    t = s.astype(np.int64)
+    t0 = t[:, 0][t[:, 0] > 0].min()
+    for name, col in (("seed_in", 2), ("idle", 4), ("lead", 5), ("done", 13), ("exit", 8)):
+        v = t[:, col]
+        v = v[v > 0]
+        if len(v):
+            out["t_" + name + "_us"] = [round(float(np.quantile((v - t0) / 100.0, x)), 1) for x in (0.0, 0.1, 0.5, 0.9, 1.0)]
     print(json.dumps(out))
     ctx.close()
 

@@ -22,10 +22,10 @@ from ppls_amd import Context, Problem  # noqa: E402
 
 # aq_stream.h ST_* order (ST_XCC = 9 holds the XCD id, not a time)
 NAMES = ["entry", "init", "seed_in", "seeded", "idle", "lead", "broke", "flushed", "exit", None,
-         "pre", "class", "feval", "done", "karg", None, None, None, None]
+         "pre", "class", "feval", "done", "karg"] + [None] * 8
 ORDER = ["entry", "karg", "pre", "init", "seed_in", "class", "feval", "seeded", "idle", "lead", "done", "broke",
          "flushed", "exit"]
-ST_XCC, ST_STRIDE = 9, 20
+ST_XCC, ST_STRIDE = 9, 24
 NW = int(os.environ.get("AQ_STAMPS_NW", "8"))   # waves per workgroup of the lone instance (aq_abi.inc AQ_LONE_NW)
 
 
