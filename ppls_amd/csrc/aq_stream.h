@@ -164,10 +164,6 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #ifndef AQ_STAMPS
 #define AQ_STAMPS 0
 #endif
-#ifndef AQ_FLUSH_LANES
-#define AQ_FLUSH_LANES 1   // the flush's slot atomics spread over lanes (flush_acc)
-#endif
-constexpr bool FLUSH_LANES = AQ_FLUSH_LANES;
 #ifndef AQ_FLUSHX
 #define AQ_FLUSHX 0   // timing experiments on the flush (stamps builds only): 1 no reductions, 2 no atomics
 #endif
@@ -561,7 +557,7 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
         const unsigned t = wave_add_full(a.tasks) + a.ut, l = wave_add_full(a.leaves) + a.ul,
                        m = max(wave_max_full(a.maxd), mdt ? (mdt & 255u) + 1u : 0u);
 #endif
-        if (AQ_FLUSHX != 2 && lane == 0 && t && (PCU || !FLUSH_LANES)) {
+        if (AQ_FLUSHX != 2 && lane == 0 && t) {
             atomicAdd(&S.tasks, (unsigned long long)t);
             if constexpr (PCU) {
                 atomicAdd(&pc[tag], (unsigned long long)t);
@@ -569,7 +565,7 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
                 atomicMax(&pc[2 * PCU_ROW + tag], (unsigned long long)m);
                 xs_atomic_add(px[tag].limb, hi);
                 xs_atomic_add(px[tag].limb, lo);
-            } else if constexpr (!FLUSH_LANES) {
+            } else {
                 Ctl& c = P.ctls[P.first_slot + tag];
                 atomicAdd(&c.sums.tasks, (unsigned long long)t);
                 atomicAdd(&c.sums.leaves, (unsigned long long)l);
@@ -577,31 +573,6 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
                 const int i0 = xs_atomic_add(c.area.limb, hi);
                 const int i1 = xs_atomic_add(c.area.limb, lo);
                 xs_window_add(c.sums, i0, i1);
-            }
-        }
-        if constexpr (!PCU && FLUSH_LANES) {
-            if (t) {
-                // the slot's atomics spread over lanes: lanes 0-2 add hi's three digits, 3-5 lo's (ONE digit
-                // split, of a per-lane input), 6 / 7 the counts, 8 the levels, 9 / 10 the limb window, 11 the
-                // workgroup's task count --
-                // three atomic instructions where lane 0 alone had issued up to eleven, each behind its
-                // own digit test (a tiny-tree flush was ~2 900 cycles, about half of it this block)
-                Ctl& c = P.ctls[P.first_slot + tag];
-                XDigits g;
-                const bool ok = xs_digits(lane < 3u ? hi : lo, g);
-                const unsigned k = lane < 3u ? lane : lane - 3u;
-                const long long dk = k == 0u ? g.d[0] : (k == 1u ? g.d[1] : g.d[2]);
-                const int i_hi = __builtin_amdgcn_readfirstlane(ok ? g.i : -1);
-                const int i_lo = __builtin_amdgcn_readlane(ok ? g.i : -1, 3);
-                if (lane < 6u && ok && dk)
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&c.area.limb[g.i + (int)k]), (unsigned long long)dk);
-                if (lane == 6u || lane == 7u)
-                    atomicAdd(lane == 6u ? &c.sums.tasks : &c.sums.leaves, (unsigned long long)(lane == 6u ? t : l));
-                const int wlo = i_hi < 0 ? i_lo : (i_lo < 0 ? i_hi : min(i_hi, i_lo)), whi = max(i_hi, i_lo);
-                if (lane == 8u) atomicMax(&c.sums.levels, m);
-                if (lane == 11u) atomicAdd(&S.tasks, (unsigned long long)t);   // (LDS: the workgroup's tasks)
-                if (wlo >= 0 && (lane == 9u || lane == 10u))
-                    atomicMax(lane == 9u ? &c.sums.win_lo_not : &c.sums.win_hi, lane == 9u ? xs_win_lo(wlo) : xs_win_hi(whi));
             }
         }
     }
