@@ -165,7 +165,8 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #define AQ_STAMPS 0
 #endif
 #ifndef AQ_FLUSHX
-#define AQ_FLUSHX 0   // timing experiments on the flush (stamps builds only): 1 no reductions, 2 no atomics
+#define AQ_FLUSHX 0   // timing experiments on the flush (stamps builds only): 1 no reductions, 2 no atomics,
+                      // 3 no double-double reduction, 4 no integer reductions
 #endif
 // Per-CU (lone) launches: a new leader first polls only its group's end flag, for up to LAZY_TICKET
 // spins, before it takes a queue ticket -- at a lone launch's end 255 leaders drawing tickets from one
@@ -231,6 +232,11 @@ constexpr unsigned TASKS_PER_JOB = AQ_TASKS_PER_JOB;   // adaptive job size: a j
 // 448 pairs at eps=1e-10 and 576 at 1e-12 (DIAG max_cellar, every workgroup, profiles/r05o); 4096 had
 // held 604 MB per context for nothing. A wave whose cellar is full spills to the pool / HBM queue.
 constexpr int CCAP = AQ_CCAP;
+#ifndef AQ_FLUSH_LDS
+#define AQ_FLUSH_LDS 0
+#endif
+// the flush sums the lanes' area digits in an LDS window instead of a double-double wave reduction
+constexpr bool FLUSH_LDS = AQ_FLUSH_LDS;
 constexpr int REFILL = WCAP - 64;   // pairs a wave with an empty ring takes back from its cellar
 #ifndef AQ_PF_BELOW
 // r02 A/B (8192-integral launch, GIVE_ROUNDS 32): 112 28.39, 96 27.93, 80 27.57, 64 27.20, 48 28.18,
@@ -539,7 +545,7 @@ struct Acc {
 // px: its LDS accumulators, one XSum per integral.
 template <int FID, bool PCU>
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, WgState& S,
-                                          unsigned long long* pc, XSum* px) {
+                                          unsigned long long* pc, XSum* px, long long* xsa, long long* xsb) {
     // (the rounds' lane partial is folded at every burst's end; fold any remainder here too)
     dd_add(a.hi, a.lo, a.r);
     a.r = 0.0;
@@ -549,14 +555,54 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
         double hi = area_scale<FID>() * a.hi, lo = area_scale<FID>() * a.lo;
 #if AQ_FLUSHX == 1   // (timing experiment only: no reductions -- wrong results)
         const unsigned t = a.ut + 1u, l = a.ul, m = 1u;
-#else
+#elif AQ_FLUSHX == 3   // (timing experiment only: no double-double reduction)
+        const unsigned mdt = wave_max_full(a.maxdt);
+        const unsigned t = wave_add_full(a.tasks) + a.ut, l = wave_add_full(a.leaves) + a.ul,
+                       m = max(wave_max_full(a.maxd), mdt ? (mdt & 255u) + 1u : 0u);
+#elif AQ_FLUSHX == 4   // (timing experiment only: no integer reductions)
         wave_sum_dd_full(hi, lo);
+        const unsigned t = a.ut + 1u, l = a.ul, m = 1u;
+#else
+        if (PCU || !FLUSH_LDS) wave_sum_dd_full(hi, lo);
         // levels: the seeds' per-lane depth + 1, and the deepest popped pair (its depth byte + 1; one
         // integral per ring, so the max over pair words is the max depth of that integral)
         const unsigned mdt = wave_max_full(a.maxdt);
         const unsigned t = wave_add_full(a.tasks) + a.ut, l = wave_add_full(a.leaves) + a.ul,
                        m = max(wave_max_full(a.maxd), mdt ? (mdt & 255u) + 1u : 0u);
 #endif
+        if constexpr (!PCU && FLUSH_LDS) {
+            if (t) {
+                // the lanes' (hi, lo) as exact digits (aq_xsum.h) into a per-wave 68-limb window in LDS --
+                // limbs 0-63 at xsa[0..63], 64-67 at xsb[0..3]: the top quarter of the wave's ring, free at
+                // every flush (the ring is empty, or holds <= REFILL pool pairs at its bottom) -- then its
+                // nonzero limbs into the slot: exact, no double-double chain, no serial digit splits
+                xsa[lane] = 0ll;
+                if (lane < 4u) xsb[lane] = 0ll;
+                auto add_digits = [&](double v) {
+                    XDigits g;
+                    if (!xs_digits(v, g)) return;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const int i = g.i + k;
+                        if (g.d[k]) atomicAdd(reinterpret_cast<unsigned long long*>(i < 64 ? &xsa[i] : &xsb[i - 64]),
+                                              (unsigned long long)g.d[k]);
+                    }
+                };
+                add_digits(area_scale<FID>() * a.hi);
+                add_digits(area_scale<FID>() * a.lo);
+                const long long v0 = xsa[lane], v1 = lane < 4u ? xsb[lane] : 0ll;
+                Ctl& c = P.ctls[P.first_slot + tag];
+                if (v0) atomicAdd(reinterpret_cast<unsigned long long*>(&c.area.limb[lane]), (unsigned long long)v0);
+                if (v1) atomicAdd(reinterpret_cast<unsigned long long*>(&c.area.limb[64 + lane]), (unsigned long long)v1);
+                const unsigned long long nz0 = __ballot(v0 != 0ll), nz1 = __ballot(v1 != 0ll);
+                if ((nz0 | nz1) && lane == 0u) {
+                    const int lo_nz = nz0 ? __builtin_ctzll(nz0) : 64 + __builtin_ctzll(nz1);
+                    const int hi_nz = nz1 ? 64 + (63 - __builtin_clzll(nz1)) : 63 - __builtin_clzll(nz0);
+                    atomicMax(&c.sums.win_lo_not, xs_win_lo(lo_nz));
+                    atomicMax(&c.sums.win_hi, (unsigned)(hi_nz + 1));
+                }
+            }
+        }
         if (AQ_FLUSHX != 2 && lane == 0 && t) {
             atomicAdd(&S.tasks, (unsigned long long)t);
             if constexpr (PCU) {
@@ -570,9 +616,11 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
                 atomicAdd(&c.sums.tasks, (unsigned long long)t);
                 atomicAdd(&c.sums.leaves, (unsigned long long)l);
                 atomicMax(&c.sums.levels, m);
-                const int i0 = xs_atomic_add(c.area.limb, hi);
-                const int i1 = xs_atomic_add(c.area.limb, lo);
-                xs_window_add(c.sums, i0, i1);
+                if constexpr (!FLUSH_LDS) {
+                    const int i0 = xs_atomic_add(c.area.limb, hi);
+                    const int i1 = xs_atomic_add(c.area.limb, lo);
+                    xs_window_add(c.sums, i0, i1);
+                }
             }
         }
     }
@@ -815,6 +863,10 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     const unsigned main_jobs = tail_from * shares_main;
     const unsigned total_jobs = main_jobs + ((unsigned)P.nprob - tail_from) * shares_tail;
     const unsigned base = wid * WCAP;                            // this wave's ring
+    // the flush's LDS digit window (FLUSH_LDS): the ring's top quarter, slots WCAP - 64 .. WCAP - 1 of its
+    // a and b fields (68 limbs), free whenever a flush runs
+    long long* const xs_a = reinterpret_cast<long long*>(s_a + base + (WCAP - 64));
+    long long* const xs_b = reinterpret_cast<long long*>(s_b + base + (WCAP - 64));
     // its LDS byte offset (the pair block is the kernel's first LDS object, and a ring is WCAP * 8 B of
     // each field: ring8 is a multiple of WCAP * 8, which ring_addr's and-or relies on)
     const unsigned ring8 = pr_base + base * 8u;
@@ -1037,7 +1089,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             }
             if (k) {
                 if (ptag != tag) {     // the ring's new integral
-                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
                     tag = ptag;
                 }
                 bot = 0;
@@ -1093,7 +1145,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 unsigned long long cf0 = 0;
                 if constexpr (AQ_STAMPS && !DIAG) cf0 = clk();
                 if (p != tag) {
-                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
                     tag = p;
                 }
                 if constexpr (AQ_STAMPS && !DIAG) {
@@ -1443,7 +1495,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             // a wave that ran dry flushes now, off the run's critical path: the workgroup's other waves
             // while its last still works; the last one (the leader) once the end is stored or while it
             // waits, below (every wave flushing after the end was seen had cost a lone launch ~1 us, r04j)
-            if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+            if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
             if (!lead) {
                 __builtin_amdgcn_s_sleep(4);
                 __builtin_amdgcn_wave_barrier();
@@ -1469,7 +1521,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             }
             // the leader's flush: behind the end's stores (the run's last leader: the other workgroups
             // see the end meanwhile), or before its wait
-            flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+            flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
             if (lane == 0) {
                 if (!last) {
                     // per-CU launches: the end flag alone first (one load per spin, no ticket)
@@ -1909,7 +1961,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
     if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_BROKE], rtc()); }
     stamp(ST_BROKE);
-    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px);
+    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
     if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_FLUSHED], rtc()); }
     stamp(ST_FLUSHED);
     if (mixed) err |= ERRB_OVERFLOW;
