@@ -355,6 +355,22 @@ def _gather(ctx, n):
     return out.cpu().numpy()
 
 
+def test_batch_order_and_host_threads_do_not_change_results(ctx, oracle, monkeypatch):
+    """Size-ordered chunks (the default) against input order (AQ_BATCH_SORT=0), and host work on
+    one thread against several (AQ_HOST_THREADS): every integral's counts identical, its area
+    within 2 ulp (another schedule of the same tree), over a two-chunk batch."""
+    n = 131072 + 5000
+    a, b = oracle.batch_bounds(n)
+    ref_area, ref_tasks, ref_acc = ctx.integrate_batch(a, b, 1e-3)
+    for env in ({"AQ_BATCH_SORT": "0"}, {"AQ_HOST_THREADS": "1"}, {"AQ_BATCH_SORT": "0", "AQ_HOST_THREADS": "3"}):
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)
+            area, tasks, acc = ctx.integrate_batch(a, b, 1e-3)
+        assert (tasks == ref_tasks).all() and (acc == ref_acc).all(), env
+        assert np.all(np.abs(area - ref_area) <= 2 * np.spacing(np.abs(ref_area))), env
+
+
 def test_max_integrals_per_launch_batch(ctx, oracle, batch_golden):
     """MAXK (262144) integrals with random bounds in ONE persistent launch (the launch shape of the
     N-GPU bench); the first 256 against the committed golden fixture, 4096 more drawn across the launch
