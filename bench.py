@@ -470,6 +470,11 @@ def main(argv=None):
     K = args.steps
     n_int = K * B
     totals = torch.zeros((n_int, 4), dtype=torch.float64, device="cuda")
+    # torch loads a kernel's code object at its first use: the column sum below (bookkeeping, not the
+    # hot path) had paid a ~25 ms one-time load inside the timed region -- 1.2 ms of every step's
+    # ms_per_step at 20 steps (rocprofv3 kernel trace, profiles/r06a: a 25.7 ms gap before the first
+    # reduce_kernel). Loaded here, untimed.
+    float(totals[:, 1].sum().item())
     ctx.kernel_timing(True)
     barrier()
     torch.cuda.synchronize()

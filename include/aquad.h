@@ -93,8 +93,9 @@ const char *aq_strerror(int code);
 /* Compute units of the context's device (one persistent workgroup each). */
 int aq_ctx_num_cus(const aq_ctx *ctx);
 /* Wavefront workers of the on-device farmer (workgroups x 12 waves per workgroup): the partition of
- * sharded and multi-integral launches (aq_integrate_shard documents it). An unsharded lone integral
- * runs 8 waves per workgroup (its set-up and seeding are issue-bound at three waves per SIMD). */
+ * sharded and multi-integral launches (aq_integrate_shard documents it). An unsharded launch of ONE
+ * integral runs 8 waves per workgroup (its set-up and seeding are issue-bound at three waves per SIMD);
+ * launches of 2 or more integrals run 12. */
 int aq_ctx_num_workers(const aq_ctx *ctx);
 /* Device memory the context holds, bytes. */
 int aq_ctx_device_bytes(const aq_ctx *ctx, uint64_t *bytes);

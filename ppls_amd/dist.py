@@ -126,17 +126,19 @@ def integrate_distributed(problem: Problem, group=None, ctx: Optional[Context] =
             torch.cuda.set_device(local_rank())
         ctx = Context(local_rank())
         own = True
-    dev = comm_device(group, ctx if shard_fn is None else None) if (nccl or shard_fn is None) else torch.device("cpu")
     row, err = np.zeros(ROW, np.int64), 0
-    if shard_fn is None:
-        _agree_on_workers(ctx.num_workers, dev, group)
+    # (the partition check can raise: a context this call created is closed on that path too)
     try:
+        dev = comm_device(group, ctx if shard_fn is None else None) if (nccl or shard_fn is None) else torch.device("cpu")
         if shard_fn is None:
-            row = ctx.integrate_shard_exact(problem, rank, world)   # internal slot: async slots untouched
-        else:
-            row = np.asarray(shard_fn(problem, rank, world), np.int64)
-    except AquadError as e:
-        err = e.code if e.code else -1
+            _agree_on_workers(ctx.num_workers, dev, group)
+        try:
+            if shard_fn is None:
+                row = ctx.integrate_shard_exact(problem, rank, world)   # internal slot: async slots untouched
+            else:
+                row = np.asarray(shard_fn(problem, rank, world), np.int64)
+        except AquadError as e:
+            err = e.code if e.code else -1
     finally:
         if own:
             ctx.close()

@@ -229,3 +229,39 @@ def test_gloo_batch_ranks_on_different_partitions_raise():
     different partitions into wrong counts."""
     results = _run(_workers_worker, 2, timeout=120)
     assert all("disagree" in results[r] for r in range(2)), results
+
+
+def _own_ctx_worker(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        import ppls_amd.dist as D
+        from ppls_amd.aquad import AquadError, Problem
+        closed = []
+
+        class _FakeContext:
+            """Stands in for the Context integrate_distributed creates itself (own=True): it disagrees
+            on the worker count across the ranks and records its close()."""
+            def __init__(self, device):
+                self.device = device
+                self.num_workers = 3072 if rank == 0 else 2048
+
+            def close(self):
+                closed.append(True)
+
+        D.Context = _FakeContext
+        try:
+            D.integrate_distributed(Problem(eps=1e-6))
+            q.put((rank, ("no error", closed)))
+        except AquadError as e:
+            q.put((rank, (str(e), closed)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_own_context_closed_when_partitions_disagree():
+    """a Context integrate_distributed created itself is closed when the partition check
+    raises (it used to leak ~1.3 GiB of device memory per rank on that path)."""
+    results = _run(_own_ctx_worker, 2, timeout=120)
+    for r in range(2):
+        msg, closed = results[r]
+        assert "disagree" in msg and closed == [True], results
