@@ -164,6 +164,12 @@ constexpr int SKEWED_GIVE_MIN = AQ_SKEWED_GIVE_MIN;
 #ifndef AQ_STAMPS
 #define AQ_STAMPS 0
 #endif
+#ifndef AQ_X_NOFOLD
+#define AQ_X_NOFOLD 0   // timing experiments only (wrong areas): per-CU launches skip the exit's area fold
+#endif
+#ifndef AQ_X_NOCUACC
+#define AQ_X_NOCUACC 0  // timing experiments only: no per-CU task counter atomic at exit
+#endif
 #ifndef AQ_FLUSHX
 #define AQ_FLUSHX 0   // timing experiments on the flush (stamps builds only): 1 no reductions, 2 no atomics,
                       // 3 no double-double reduction, 4 no integer reductions
@@ -1989,7 +1995,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             // per-CU task counters on every launch shape: the workgroup's tasks, once,
             // into its hardware CU slot -- one atomic per workgroup and launch, on 256 distinct lines
             const unsigned long long wt = __hip_atomic_load(&S.tasks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (wt) __hip_atomic_fetch_add(&P.cu_acc[cu_slot()], wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wt && !AQ_X_NOCUACC) __hip_atomic_fetch_add(&P.cu_acc[cu_slot()], wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if constexpr (DIAG) { if (last) atomicMax(&s_dg[DG_T_FOLD], rtc()); }
         if (PCU && last) {
@@ -2026,7 +2032,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             }
         }
     }
-    if constexpr (PCU) {
+    if constexpr (PCU && !AQ_X_NOFOLD) {
         // the workgroup's last wave folds the workgroup's exact area accumulators into the slots:
         // one lane per limb, only the non-zero limbs (a handful per integral)
         if (uni(__shfl(last_u, 0, 64))) {
