@@ -73,7 +73,7 @@ typedef struct {
     uint32_t levels;    /* 1 + deepest refinement level reached */
     uint32_t n_cu;      /* CUs that evaluated at least one task. Per-CU counts (n_cu, tasks_per_cu) are kept
                            for the synchronous calls and for launches of fewer than 12 integrals into slots
-                           below 65536; other launches report n_cu = 0 and zero rows (their per-CU work is
+                           below 16384; other launches report n_cu = 0 and zero rows (their per-CU work is
                            still counted by aq_cu_task_counters, which sees every launch) */
     uint64_t spilled;   /* interval pairs moved through the HBM work queue (load balance) */
     uint32_t n_gpus;    /* GPUs that contributed (entries written to tasks_per_gpu) */

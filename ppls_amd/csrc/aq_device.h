@@ -331,6 +331,17 @@ __device__ __forceinline__ unsigned wave_max_full(unsigned v) {
 __device__ __forceinline__ unsigned wave_or_full(unsigned v) {
     return wave_reduce_u(v, [](unsigned x, unsigned y) { return x | y; });
 }
+// double-double sum over each row of 16 lanes (every lane active): every lane holds its row's sum
+__device__ __forceinline__ void row_sum_dd(double& hi, double& lo) {
+    double h2 = dpp_d<DPP_XOR1>(hi), l2 = dpp_d<DPP_XOR1>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    h2 = dpp_d<DPP_XOR2>(hi); l2 = dpp_d<DPP_XOR2>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    h2 = dpp_d<DPP_HALF_MIRROR>(hi); l2 = dpp_d<DPP_HALF_MIRROR>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+    h2 = dpp_d<DPP_MIRROR>(hi); l2 = dpp_d<DPP_MIRROR>(lo);
+    dd_add_dd(hi, lo, h2, l2);
+}
 // double-double sum over the wave (every lane active); the result is wave-uniform
 __device__ __forceinline__ void wave_sum_dd_full(double& hi, double& lo) {
     double h2 = dpp_d<DPP_XOR1>(hi), l2 = dpp_d<DPP_XOR1>(lo);

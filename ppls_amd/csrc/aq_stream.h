@@ -85,6 +85,14 @@ constexpr unsigned GSS_DIV = AQ_GSS_DIV;
 #ifndef AQ_S_W1
 #define AQ_S_W1 2
 #endif
+#ifndef AQ_HEAP_SEED
+#define AQ_HEAP_SEED 1
+#endif
+// whole-integral jobs (V = 1) seed the top HEAP_D + 1 levels, one node per lane in heap order (k_stream)
+constexpr bool HEAP_SEED = AQ_HEAP_SEED != 0;
+constexpr int HEAP_D = 4;
+constexpr unsigned HEAP_NODES = (2u << HEAP_D) - 1u;   // 31 nodes + F(A), F(B): 33 lanes
+static_assert(HEAP_NODES + 2u <= 64u, "the heap seeding path is one node per lane");
 // seed depth of a job: floor(log2 V) + S_W for V = shares x shards virtual workers; a whole-integral
 // job (V = 1, tiny trees of big batches) seeds at S_W1 (its partition is the whole tree at any depth)
 __host__ __device__ constexpr int seed_depth(unsigned long long V) {
@@ -211,7 +219,15 @@ __host__ __device__ constexpr unsigned dt_tag(unsigned dt) { return (dt >> TAG_S
 constexpr int MAXK = 1 << 18;
 static_assert((unsigned)MAXK - 1u <= TAG_MASK, "the tag field must hold every integral of a launch");
 // slots whose per-CU launches keep per-workgroup words (parts), plus one row for the sync slot
-constexpr int NPARTS = 65536;
+// PCU_AREA: a per-CU launch's area is kept per workgroup -- each wave adds its flushes' double-doubles
+// into its own LDS pair per integral (flush_acc), the workgroup's last wave sums its waves' into two
+// doubles beside the count words (StreamParams::parea) -- and readers add the grid's pairs into the slot's
+// exact accumulator: k_fold_parts after an asynchronous per-CU launch, k_fetch_sync / k_pack_group on the
+// synchronous and group paths. So the area of a lone integral is the correctly rounded sum of 2 x grid
+// doubles, each a double-double of its workgroup's waves' partials (no far atomic at the launch's end).
+// (r06: 16384, was 65536 -- with the per-workgroup area words beside the counts, PCU_AREA, the two blocks
+// take 134 MB where the counts alone took 268 MB)
+constexpr int NPARTS = 16384;
 __host__ __device__ __forceinline__ size_t parts_row(int slot) { return slot < NPARTS ? (size_t)slot : (size_t)NPARTS; }
 #ifndef AQ_GSPLIT_DEFAULT
 // sharded launches / first launch: 16 shares per integral over all shards (2-rank rehearsal, r03: 32 ->
@@ -438,6 +454,8 @@ struct StreamParams {
     QCtl* q_next;                   // the next launch's: workgroup 0 zeroes it
     unsigned long long* parts;      // per-CU launches' counts (slot_counts): integral p's row at
                                     // [2 * (p * gridDim.x + wg) + 0/1] (the first slot's parts row)
+    double* parea;                  // ... and their area, a double-double per workgroup at [2 * (p * gridDim.x
+                                    // + wg) + 0/1] (the same row of the area words; PCU_AREA)
     unsigned long long* diag;       // optional per-workgroup timeline (DIAG_WORDS each)
     unsigned long long* cu_acc;     // [AQ_CU_SLOTS] tasks per hardware CU slot, summed over launches
                                     // (every launch: the farmer's tasks_per_process, :162, per CU)
@@ -551,7 +569,8 @@ struct Acc {
 // px: its LDS accumulators, one XSum per integral.
 template <int FID, bool PCU>
 __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag, unsigned lane, WgState& S,
-                                          unsigned long long* pc, XSum* px, long long* xsa, long long* xsb) {
+                                          unsigned long long* pc, double2* wdd, int wdd_stride, long long* xsa,
+                                          long long* xsb) {
     // (the rounds' lane partial is folded at every burst's end; fold any remainder here too)
     dd_add(a.hi, a.lo, a.r);
     a.r = 0.0;
@@ -615,8 +634,12 @@ __device__ __forceinline__ void flush_acc(const StreamParams& P, Acc& a, int tag
                 atomicAdd(&pc[tag], (unsigned long long)t);
                 atomicAdd(&pc[PCU_ROW + tag], (unsigned long long)l);
                 atomicMax(&pc[2 * PCU_ROW + tag], (unsigned long long)m);
-                xs_atomic_add(px[tag].limb, hi);
-                xs_atomic_add(px[tag].limb, lo);
+                // the wave's own double-double of this integral (no other wave writes it): the workgroup's
+                // last wave sums the waves' at exit into the per-workgroup area words (PCU_AREA)
+                double2& w = wdd[tag * wdd_stride];
+                double wh = w.x, wl = w.y;
+                dd_add_dd(wh, wl, hi, lo);
+                w = make_double2(wh, wl);
             } else {
                 Ctl& c = P.ctls[P.first_slot + tag];
                 atomicAdd(&c.sums.tasks, (unsigned long long)t);
@@ -760,6 +783,7 @@ template <int FID, bool HIST, bool DIAG, bool PCU, int NWT = NW>
 __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     constexpr int PTT = NWT * 64;   // threads per workgroup
     static_assert(NWT >= 4 && NWT <= NW && NWT % 4 == 0, "whole waves per SIMD, within the LDS rings");
+    static_assert(NWT <= 16, "the exit's area sum runs over one DPP row of lanes (PCU_AREA)");
     // one SoA block (a | b | fa | fm | fb, LREC doubles each) so that every field of a slot is a
     // constant offset from one address (ds_read2st64 / ds_write2st64 pairs, no per-field adds). A
     // pair stores no midpoint: m = (a + b) / 2 is recomputed with the parent's own operands (:187),
@@ -784,7 +808,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     double* const s_fb = s_pr + 4 * LREC;
     __shared__ WgState S;
     __shared__ unsigned long long s_pc[PCU ? 3 * PCU_ROW : 1];
-    __shared__ XSum s_px[PCU ? PCU_ROW : 1];
+    __shared__ double2 s_wdd[PCU ? PCU_ROW * NWT : 1];   // per-CU launches: each wave's area per integral
     __shared__ unsigned long long s_dg[DIAG ? DIAG_WORDS : 1];
 
     const unsigned tid = threadIdx.x;
@@ -825,7 +849,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     }
     if (PCU && tid < 3u * PCU_ROW) s_pc[tid] = 0ull;
     if (PCU)
-        for (unsigned i = tid; i < (unsigned)(PCU_ROW * XS_LIMBS); i += PTT) s_px[i / XS_LIMBS].limb[i % XS_LIMBS] = 0;
+        for (unsigned i = tid; i < (unsigned)(PCU_ROW * NWT); i += PTT) s_wdd[i] = make_double2(0.0, 0.0);
     if (DIAG) {
         for (unsigned i = tid; i < DIAG_WORDS; i += PTT) s_dg[i] = (i == DG_T_FIRST_LEAD) ? ~0ull : 0ull;
     }
@@ -1095,7 +1119,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             }
             if (k) {
                 if (ptag != tag) {     // the ring's new integral
-                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
+                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_wdd + wid, NWT, xs_a, xs_b);
                     tag = ptag;
                 }
                 bot = 0;
@@ -1151,7 +1175,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 unsigned long long cf0 = 0;
                 if constexpr (AQ_STAMPS && !DIAG) cf0 = clk();
                 if (p != tag) {
-                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
+                    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_wdd + wid, NWT, xs_a, xs_b);
                     tag = p;
                 }
                 if constexpr (AQ_STAMPS && !DIAG) {
@@ -1205,7 +1229,66 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 bool alive = false, alive2 = false;   // alive2: the dual path's second node per lane
                 double l = A, r = B, fl = 0.0, fr = 0.0, mid = 0.0, fmid = 0.0;
                 double l2 = A, r2 = B, fl2 = 0.0, fr2 = 0.0, fmid2 = 0.0;
-                if (nnodes <= 64) {
+                // the depth of the seeded pairs' parents (the heap path seeds one level deeper)
+                int Ds = D;
+                if (HEAP_SEED && V == 1u) {
+                    // Whole-integral job (V = 1: the wave owns the whole tree, tiny trees of big batches).
+                    // Lane q < 31 owns node q of the top five levels in heap order (depth d = log2(q + 1),
+                    // k = q + 1 - 2^d), lanes 31 / 32 F(A) / F(B): every node ONCE, where the column path's
+                    // 32 lanes evaluate the 15 nodes of four levels (each node once per position below it).
+                    // One F per lane either way, and the first burst starts with up to 16 pairs instead of
+                    // 8 -- one ramp round fewer per tiny tree (C3 at eps=1e-3: ~14 rounds of ~1 400 tasks).
+                    Ds = HEAP_D;
+                    const unsigned q = lane;
+                    const bool isnode = q < HEAP_NODES;
+                    const unsigned d = isnode ? 31u - (unsigned)__builtin_clz(q + 1u) : 0u;
+                    const unsigned k = isnode ? q + 1u - (1u << d) : 0u;
+                    unsigned li = HEAP_NODES, ri = HEAP_NODES + 1u;
+                    for (unsigned i = 0; i < d; ++i) {
+                        const double mm = (l + r) / 2;                           // :187 on the path
+                        const unsigned anc = (1u << i) - 1u + (k >> (d - i));    // the path's node at depth i
+                        if ((k >> (d - 1u - i)) & 1u) { l = mm; li = anc; } else { r = mm; ri = anc; }
+                    }
+                    mid = (l + r) / 2;                                            // :187
+                    if (q < HEAP_NODES + 2u) {
+                        fmid = integrand<FID>(isnode ? mid : (q == HEAP_NODES ? A : B), tab);   // :188
+                        fm[q] = fmid;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    bool refine = false;
+                    double leafarea = 0.0;
+                    if (isnode) {
+                        fl = fm[li];
+                        fr = fm[ri];
+                        const double lrarea = (fl + fr) * (r - l) / 2;        // :185
+                        const double larea = (fl + fmid) * (mid - l) / 2;     // :189
+                        const double rarea = (fmid + fr) * (r - mid) / 2;     // :190
+                        refine = fabs((larea + rarea) - lrarea) > eps;       // :191
+                        leafarea = larea + rarea;                             // :199
+                    }
+                    // a node is a task of the tree iff every ancestor refines (:192-197)
+                    const unsigned long long rm = __ballot(isnode && refine);
+                    bool ev = isnode;
+                    for (unsigned x = q; ev && x > 0u;) {
+                        x = (x - 1u) >> 1;
+                        ev = ((rm >> x) & 1ull) != 0ull;
+                    }
+                    if (ev) {
+                        ++acc.tasks;
+                        acc.maxd = max(acc.maxd, d + 1u);
+                        if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[d], 1ull);
+                        if (!refine) {
+                            dd_add(acc.hi, acc.lo, leafarea / area_scale<FID>());   // :199 -> :149 (doubled, exact)
+                            ++acc.leaves;
+                            if (HIST) atomicAdd(&P.ctls[P.first_slot + p].hist[AQ_MAX_LEVELS + d], 1ull);
+                        } else if ((int)d + 1 >= max_depth) {
+                            err |= ERRB_DEPTH;
+                        }
+                    }
+                    alive = ev && refine && d == (unsigned)HEAP_D && HEAP_D + 1 < max_depth;
+                    if (burst_cap && alive) acc.maxd = max(acc.maxd, (unsigned)HEAP_D + 2u);
+                    if constexpr (DIAG) { cp1 = clk(); cp2 = cp1; }
+                } else if (nnodes <= 64) {
                     // fast path: lane q = d*nb + kk owns node (d, kk) -- its path walk, its F(mid), its
                     // decision; the first leaf depth of every position comes from ONE ballot
                     unsigned long long ca = 0, cb = 0;
@@ -1453,7 +1536,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                     // a pair holds its endpoints halved (aq_device.h pair_step_halves; exact)
                     s_a[j] = 0.5 * l; s_b[j] = 0.5 * r; s_fa[j] = fs * fl; s_fm[j] = fs * fmid; s_fb[j] = fs * fr;   // :192-197
                     const bool span = FID == F_COSH4 && cosh_main_span(l, r);
-                    s_dt[j] = (unsigned)(D + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
+                    s_dt[j] = (unsigned)(Ds + 1) | (span ? SPAN_BIT : 0u) | ((unsigned)p << TAG_SHIFT);
                 }
                 unsigned n_seeds = (unsigned)__popcll(am);
                 if constexpr (FID == F_SIN_RECIP) {   // the dual path's second nodes
@@ -1501,7 +1584,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             // a wave that ran dry flushes now, off the run's critical path: the workgroup's other waves
             // while its last still works; the last one (the leader) once the end is stored or while it
             // waits, below (every wave flushing after the end was seen had cost a lone launch ~1 us, r04j)
-            if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
+            if (counted_now) flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_wdd + wid, NWT, xs_a, xs_b);
             if (!lead) {
                 __builtin_amdgcn_s_sleep(4);
                 __builtin_amdgcn_wave_barrier();
@@ -1527,7 +1610,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
             }
             // the leader's flush: behind the end's stores (the run's last leader: the other workgroups
             // see the end meanwhile), or before its wait
-            flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
+            flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_wdd + wid, NWT, xs_a, xs_b);
             if (lane == 0) {
                 if (!last) {
                     // per-CU launches: the end flag alone first (one load per spin, no ticket)
@@ -1967,7 +2050,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     // ---------------- exit: flush this wave's accumulators (no workgroup barrier needed) --------
     if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_BROKE], rtc()); }
     stamp(ST_BROKE);
-    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_px, xs_a, xs_b);
+    flush_acc<FID, PCU>(P, acc, tag, lane, S, s_pc, s_wdd + wid, NWT, xs_a, xs_b);
     if constexpr (DIAG) { if (lane == 0) atomicMax(&s_dg[DG_T_FLUSHED], rtc()); }
     stamp(ST_FLUSHED);
     if (mixed) err |= ERRB_OVERFLOW;
@@ -2033,19 +2116,26 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
         }
     }
     if constexpr (PCU && !AQ_X_NOFOLD) {
-        // the workgroup's last wave folds the workgroup's exact area accumulators into the slots:
-        // one lane per limb, only the non-zero limbs (a handful per integral)
+        // the workgroup's last wave: the waves' double-doubles of each integral summed (lanes < NWT, one
+        // DPP row) into the workgroup's two area words, plain stores beside its count words. Readers add
+        // the grid's words exactly (k_fold_parts, k_fetch_sync, k_pack_group). r06: the workgroups had
+        // folded an exact LDS accumulator into the slot with far atomics at exit -- ~1 300 atomics on the
+        // same one or two limb lines at the launch's end, 2.6 us of a 21 us lone integral (profiles/r06b:
+        // the AQ_X_NOFOLD timing build; moving them to the waiting leaders saved nothing, r06c)
         if (uni(__shfl(last_u, 0, 64))) {
             for (int p = 0; p < P.nprob; ++p) {
-                long long* g = P.ctls[P.first_slot + p].area.limb;
-                for (unsigned i = lane; i < (unsigned)XS_LIMBS; i += 64) {
-                    const long long v = (long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(&s_px[p].limb[i]),
-                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&g[i]), (unsigned long long)v);
+                double hi = 0.0, lo = 0.0;
+                if (lane < (unsigned)NWT) {
+                    const double2 w = s_wdd[p * NWT + (int)lane];
+                    hi = w.x;
+                    lo = w.y;
                 }
-                // (the slot's limb window is the whole accumulator, stored once below by workgroup 0: 256
-                // workgroups folding two more atomics each into the sums line at the launch's end had
-                // cost a lone integral ~3 us, profiles/r05d)
+                row_sum_dd(hi, lo);   // lanes 0-15 (NWT <= 16): every lane of the row holds the sum
+                if (lane == 0) {
+                    double* pa = P.parea + 2 * ((size_t)p * gridDim.x + bid);
+                    pa[0] = hi;
+                    pa[1] = lo;
+                }
             }
         }
     }

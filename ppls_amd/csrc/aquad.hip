@@ -677,6 +677,35 @@ __global__ __launch_bounds__(64) void k_gather_exact(const Ctl* __restrict__ ctl
     }
 }
 
+// PCU_AREA (aq_stream.h): add the exact sum of a per-CU launch's workgroup area words -- 2 x grid doubles,
+// one double-double per workgroup -- to sx[XS_LIMBS] (block-shared). Every thread of the block calls it
+// between barriers; LDS int64 atomics keep the sum exact in any order.
+__device__ __forceinline__ void add_wg_area(long long* sx, const double* __restrict__ pa, int grid) {
+    for (int i = threadIdx.x; i < 2 * grid; i += blockDim.x) {
+        XDigits g;
+        if (xs_digits(pa[i], g)) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (g.d[k]) atomicAdd(reinterpret_cast<unsigned long long*>(&sx[g.i + k]), (unsigned long long)g.d[k]);
+        }
+    }
+}
+
+// After an asynchronous per-CU launch of k integrals (slots first .. first + k - 1; pa: the launch's area
+// row, integral b's words at pa + 2 * b * grid): each slot's workgroup areas into its exact accumulator,
+// one workgroup per slot -- every reader (k_gather*, aq_fetch*) then sees the whole area in the slot.
+__global__ __launch_bounds__(256) void k_fold_parts(Ctl* __restrict__ ctls, const double* __restrict__ pa, int grid,
+                                                    int first) {
+    __shared__ long long sx[XS_LIMBS];
+    for (int i = threadIdx.x; i < XS_LIMBS; i += blockDim.x) sx[i] = 0;
+    __syncthreads();
+    add_wg_area(sx, pa + 2 * (size_t)blockIdx.x * grid, grid);
+    __syncthreads();
+    Ctl& c = ctls[first + (int)blockIdx.x];
+    for (int i = threadIdx.x; i < XS_LIMBS; i += blockDim.x)
+        if (sx[i]) c.area.limb[i] += sx[i];
+}
+
 // Return slots [first, first + n) to the all-zero state a launch needs: sums and the exact area
 // accumulator; the histograms when they were written.
 __global__ __launch_bounds__(128) void k_reset(Ctl* __restrict__ ctls, int first, int zero_hist) {
@@ -700,11 +729,17 @@ struct SyncOut {
     unsigned long long hist[2 * AQ_MAX_LEVELS];
     unsigned long long parts[2 * MAXG];
 };
-__global__ __launch_bounds__(256) void k_fetch_sync(Ctl* __restrict__ c, unsigned long long* __restrict__ parts, int grid,
-                                                    int with_parts, int with_hist, SyncOut* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_fetch_sync(Ctl* __restrict__ c, unsigned long long* __restrict__ parts,
+                                                    const double* __restrict__ parea, int grid, int with_parts,
+                                                    int with_hist, SyncOut* __restrict__ out) {
     const int t = threadIdx.x;
+    __shared__ long long sx[XS_LIMBS];
     if (t == 0) out->sums = c->sums;
-    for (int i = t; i < XS_LIMBS; i += blockDim.x) out->area.limb[i] = c->area.limb[i];
+    for (int i = t; i < XS_LIMBS; i += blockDim.x) sx[i] = c->area.limb[i];
+    __syncthreads();
+    if (with_parts) add_wg_area(sx, parea, grid);   // a per-CU launch's workgroup areas (PCU_AREA)
+    __syncthreads();
+    for (int i = t; i < XS_LIMBS; i += blockDim.x) out->area.limb[i] = sx[i];
     if (with_hist)
         for (int i = t; i < 2 * AQ_MAX_LEVELS; i += blockDim.x) out->hist[i] = c->hist[i];
     if (with_parts)
@@ -722,11 +757,16 @@ __global__ __launch_bounds__(256) void k_fetch_sync(Ctl* __restrict__ c, unsigne
 // ranks): limbs, tasks, accepted, spilled. info (gathered from every rank): tasks, levels, error,
 // then the rank's per-workgroup pack_cu words (grid of them; zero when not kept).
 __global__ __launch_bounds__(256) void k_pack_group(const Ctl* __restrict__ ctls, const unsigned long long* parts,
-                                                    int slot, int grid, int with_parts, long long* __restrict__ sum_row,
-                                                    unsigned long long* __restrict__ info) {
+                                                    const double* __restrict__ parea, int slot, int grid, int with_parts,
+                                                    long long* __restrict__ sum_row, unsigned long long* __restrict__ info) {
     const Ctl& c = ctls[slot];
     const unsigned long long* wp = parts + 2 * parts_row(slot) * grid;
-    for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) sum_row[k] = c.area.limb[k];
+    __shared__ long long sx[XS_LIMBS];
+    for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) sx[k] = c.area.limb[k];
+    __syncthreads();
+    if (with_parts) add_wg_area(sx, parea + 2 * parts_row(slot) * grid, grid);   // PCU_AREA
+    __syncthreads();
+    for (int k = threadIdx.x; k < XS_LIMBS; k += blockDim.x) sum_row[k] = sx[k];
     for (int k = threadIdx.x; k < grid; k += blockDim.x) info[3 + k] = with_parts ? wp[2 * k] : 0ull;
     if (threadIdx.x == 0) {
         const Counts k = slot_counts(c.sums, wp, grid);

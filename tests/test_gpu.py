@@ -326,23 +326,29 @@ def test_cu_task_counters_every_launch(ctx, trees):
 
 def test_small_launches_in_high_slots(ctx, trees):
     """launches of fewer than 12 integrals run the per-CU instance only while their
-    slots lie below 65536 (the per-workgroup words exist for those); at first_slot 65531 with 11
-    integrals (straddling the boundary), 200000 and the last slot, they run the bulk instance with a
-    static job stride. Counts exact and areas within 1e-12 everywhere; the per-CU row is kept below
-    65536 and documented as absent above (n_cu = 0, include/aquad.h) -- the context's per-CU counters
-    (aq_cu_task_counters) count every launch either way."""
+    slots lie below NPARTS = 16384 (the per-workgroup words exist for those; 65536 before r06); at
+    first_slot 16373 with 11 integrals (the last per-CU slots), 16380 with 11 (straddling the boundary),
+    65531, 200000 and the last slot, they run the bulk instance with a static job stride. Counts exact and
+    areas within 1e-12 everywhere -- the per-CU instance's area through its per-workgroup words
+    (PCU_AREA, folded by k_fold_parts) -- and within one ulp of the leaf sum for the per-CU ones; the
+    per-CU row is kept below NPARTS and documented as absent above (n_cu = 0, include/aquad.h) -- the
+    context's per-CU counters (aq_cu_task_counters) count every launch either way."""
     g = trees["cosh4_eps1e-8"]
+    nparts = 16384
     ctx.set_level_histograms(False)
     try:
-        for first, k in [(65531, 1), (65531, 11), (200000, 1), (200000, 11), (ctx.async_slots - 1, 1)]:
+        for first, k in [(0, 3), (16373, 11), (16380, 11), (65531, 1), (65531, 11), (200000, 1), (200000, 11),
+                         (ctx.async_slots - 1, 1)]:
             ctx.cu_task_counters(reset=True)
             ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), 1e-8, first_slot=first)
             for i in range(k):
                 r = ctx.fetch(first + i, detail=True)
                 assert (r.tasks, r.accepted) == (g["tasks"], g["leaves"]), (first, k, i)
                 assert _area_ok(r.area, g["area_quad"]), (first, k, i)
-                if first + k <= 65536:
+                if first + k <= nparts:
                     assert r.n_cu >= 1 and sum(r.tasks_per_cu.values()) == r.tasks
+                    want = float(g["area_quad"])
+                    assert abs(r.area - want) <= math.ulp(want), (first, k, i, r.area.hex(), want.hex())
                 else:
                     assert r.n_cu == 0 and r.tasks_per_cu == {}
             assert sum(ctx.cu_task_counters(reset=True).values()) == k * g["tasks"]
@@ -669,7 +675,8 @@ def test_plugin_reference_printout(ctx, trees):
 def test_context_footprint():
     """No per-wave area partials or second engine: a fresh context holds ~1.3 GiB -- 262144 result
     slots (738 MB, r04: 8 x 32768 per launch), the wave cellars (302 MB: 2048 pairs each since r05,
-    from 4096), the per-CU words of the first 65536 slots (268 MB) and the HBM queue -- of the GPU's
+    from 4096), the per-CU count and area words of the first 16384 slots (134 MB; r05: counts of 65536,
+    268 MB) and the HBM queue -- of the GPU's
     288 GB (round 1: ~7 GiB; the level path's two 512 MiB frontiers are allocated only when
     aq_integrate_levels first runs)."""
     from ppls_amd import Context
