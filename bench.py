@@ -15,7 +15,7 @@ ONE all-reduce inside the timed region. Launches are pipelined
 (no host sync between them); every integral's counts are verified bit-exactly and its area to
 1e-12 relative against the golden tree after timing.
 
-After the headline's timed region, three secondary passes are timed the same way (barrier + sync on
+After the headline's timed region, four secondary passes are timed the same way (barrier + sync on
 both sides, max over ranks) and reported under "secondary":
   * C3 (BASELINE configs[2]): 1 000 000 splitmix64-bounded integrals at EPSILON=1e-10, split into
     contiguous whole-integral blocks per rank, through the batch front end (aq_integrate_batch);
@@ -23,6 +23,9 @@ both sides, max over ranks) and reported under "secondary":
     (Σ leaves of the first 10 000 draws, tests/golden/batch.json);
   * C5 (BASELINE configs[4]): EPSILON=1e-12, 4096 copies of the integral per pass, each sharded over
     the N GPUs; verified against the golden tree (counts exact, area to 1e-12);
+  * C4 (BASELINE configs[3]): sin(1/x) on [1e-4, 1] at EPSILON=1e-9, 4096 copies per pass as whole
+    integrals in contiguous blocks per rank, and the lone integral's kernel time; verified against the
+    golden sin(1/x) tree;
   * C3 again at EPSILON=1e-3 (SURVEY §8d's launch/compaction-bound run: ~1 400 tasks per integral),
     verified the same way (the first 256 integrals, the 10 000-draw KAT: mean leaves 711.4936).
 
@@ -60,6 +63,8 @@ GOLDEN = {1e-10: (1464273, 732137, 7583461.361505481304452902),
 AREA_RTOL = 1e-12           # the north star's area tolerance
 C3_N = 1_000_000
 C5_COPIES = 4096
+C4_COPIES = 4096
+C4 = (1e-4, 1.0, 1e-9)      # BASELINE configs[3]: sin(1/x) on [1e-4, 1] at EPSILON=1e-9
 SPLITMIX_GOLDEN = 0x9E3779B97F4A7C15
 CPU_ENV = "BENCH_CPU_BASELINE"   # the launcher's CPU baseline, handed to rank 0 (JSON)
 
@@ -535,6 +540,7 @@ def main(argv=None):
         secondary = [
             c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist),
             c5_pass(ctx, rank, world, barrier, launch, reduce_list, dist, torch, all_reduce),
+            c4_pass(ctx, rank, world, barrier, in_turn, reduce_list, dist, torch),
             c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist, eps=1e-3),
         ]
         ok = ok and all(s["verified"] for s in secondary)
@@ -613,6 +619,69 @@ def c3_pass(ctx, args, rank, world, barrier, in_turn, reduce_list, dist, eps=1e-
             "integrals_per_s": n / elapsed, "accepted": int(leaves), "tasks": int(tsum),
             "frac": FLOP_PER_TASK * tsum / ksum / FP64_PEAK if ksum > 0 else None,
             "verified": okall == world, "checks": ["T = 2L - 1 for every integral"] + checked}
+
+
+def c4_pass(ctx, rank, world, barrier, in_turn, reduce_list, dist, torch):
+    """BASELINE configs[3]: sin(1/x) on [1e-4, 1] at EPSILON=1e-9 (the skewed tree: nearly all of its
+    56 357 tasks lie in one small region near 1e-4). C4_COPIES copies per pass as WHOLE integrals in
+    contiguous blocks per rank -- its per-integral shards are seeding-bound, whole trees are not
+    (a batch of config-4 integrals is distributed as whole integrals) -- one untimed launch
+    that sizes the jobs, two timed; and the lone integral's kernel time (the synchronous call, 8
+    launches). Verified: every copy's counts exact and area within 1e-12 of the golden tree's quad Σ
+    (tests/golden/trees.json, pinned by the reference binary built with that F)."""
+    import numpy as np
+    from ppls_amd import Problem, SIN_RECIP
+    a0, b0, eps = C4
+    g = (load_json(os.path.join("tests", "golden", "trees.json")) or {}).get("sin_recip_eps1e-9") or {}
+    m = C4_COPIES
+    lo, hi = rank * m // world, (rank + 1) * m // world
+    mine = hi - lo
+    A, B = np.full(mine, a0), np.full(mine, b0)
+
+    def run():
+        ctx.integrate_many_async(A, B, eps, first_slot=0, integrand=SIN_RECIP)
+
+    in_turn(run)                        # untimed: sizes the jobs (the launch-to-launch hint)
+    ctx.synchronize()
+    reps = 2
+    rows = torch.zeros((reps * max(mine, 1), 4), dtype=torch.float64, device="cuda")
+    ctx.kernel_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        in_turn(run)
+        ctx.gather_results(0, mine, rows.data_ptr() + i * mine * 4 * rows.element_size())
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    kern_ms, launches = ctx.kernel_time()
+    ctx.kernel_timing(False)
+    tot = rows.cpu().numpy()[:reps * mine]
+    ok = bool(g) and bool((tot[:, 3] == 0).all() and (tot[:, 1] == g["tasks"]).all() and
+                          (tot[:, 2] == g["leaves"]).all()) and areas_ok(tot[:, 0], float(g["area_quad"]))
+    # the lone integral (one launch per integral, on every rank)
+    p = Problem(SIN_RECIP, a0, b0, eps)
+    ctx.integrate(p)
+    ctx.kernel_timing(True)
+    for _ in range(8):
+        r = ctx.integrate(p)
+    lone_ms, lone_n = ctx.kernel_time()
+    ctx.kernel_timing(False)
+    ok = ok and bool(g) and (r.tasks, r.accepted) == (g["tasks"], g["leaves"])
+    elapsed, lone_us = reduce_list([t1 - t0, lone_ms * 1e3 / max(lone_n, 1)], dist.ReduceOp.MAX)
+    leaves, tasks, okall = reduce_list([float(tot[:, 2].sum()), float(tot[:, 1].sum()), 1.0 if ok else 0.0],
+                                       dist.ReduceOp.SUM)
+    return {"workload": "C4 (BASELINE configs[3]): sin(1/x) on [1e-4,1] at EPSILON=1e-9, %d copies per pass as whole "
+                        "integrals in contiguous blocks per rank, %d timed passes; and one integral per launch" % (m, reps),
+            "value": leaves / elapsed, "unit": "accepted subintervals/s", "ms": elapsed * 1e3,
+            "tasks_per_s": tasks / elapsed, "integrals_per_s": reps * m / elapsed,
+            "single_integral_kernel_us": lone_us,
+            "frac": None, "frac_note": "no algorithmic FLOP count is defined for glibc sin's range paths "
+                                       "(SURVEY §8d defines 38 per task for cosh4 only)",
+            "verified": okall == world,
+            "checks": ["counts exact and areas to 1e-12 vs the golden sin(1/x) tree, every copy and the lone integral"]}
 
 
 def c5_pass(ctx, rank, world, barrier, launch, reduce_list, dist, torch, all_reduce):
