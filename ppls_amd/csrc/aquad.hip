@@ -338,15 +338,6 @@ constexpr int LEVEL_T = AQ_LEVEL_T;
 #define AQ_LEVEL_HOIST 0   // r03 A/B (profiles/r03q/front_ab.txt): widest level 32.4 -> 35.4 us with it -- off
 #endif
 constexpr int LEVEL_NW = LEVEL_T / 64;
-#ifndef AQ_LEVEL_PF
-#define AQ_LEVEL_PF 1
-#endif
-// r06: the grid is the resident capacity (occupancy x CUs, level_step_impl), each block runs several
-// chunks and loads the next chunk's records while this one's F chains run; a block with no chunk
-// skips the table staging (the chained levels are launched for the buffer's capacity). r02-r05's one
-// chunk per block (1612 blocks at the widest level, ~1.6 rounds of resident blocks) was bound by each
-// block's latency chain: table, loads, F, append atomic, stores.
-constexpr bool LEVEL_PF = AQ_LEVEL_PF != 0;
 
 template <int FID>
 __global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ in, unsigned n_in, Rec* __restrict__ out,
@@ -376,11 +367,9 @@ __global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ 
             rn[k] = an[k] ? in[i] : Rec{1.0, 1.0, 0.0, 0.0};
         }
     };
-    const bool work = blockIdx.x * chunk < n_in;   // block-uniform
-    if (AQ_LEVEL_HOIST && work) load_chunk(blockIdx.x * chunk);
-    if (work || !LEVEL_PF) stage_f_table<FID>(tab, gtab);
+    if (AQ_LEVEL_HOIST && blockIdx.x * chunk < n_in) load_chunk(blockIdx.x * chunk);
+    stage_f_table<FID>(tab, gtab);
     __syncthreads();
-    if (LEVEL_PF && !AQ_LEVEL_HOIST && work) load_chunk(blockIdx.x * chunk);
     double hi = 0.0, lo = 0.0;
     unsigned tasks = 0, leaves = 0, err = 0;
     const unsigned w = threadIdx.x >> 6;
@@ -390,15 +379,13 @@ __global__ __launch_bounds__(LEVEL_T) void k_level_step(const Rec* __restrict__ 
         Rec rc[R];
         bool active[R];
         double x[R], f[R];
-        if (!LEVEL_PF && (!AQ_LEVEL_HOIST || base != blockIdx.x * chunk)) load_chunk(base);
+        if (!AQ_LEVEL_HOIST || base != blockIdx.x * chunk) load_chunk(base);
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             active[k] = an[k];
             rc[k] = rn[k];
             x[k] = (rc[k].l + rc[k].r) / 2;                              // :187
         }
-        // the next chunk's records go out now: their latency overlaps this chunk's F chains
-        if (LEVEL_PF && base + gridDim.x * chunk < n_in) load_chunk(base + gridDim.x * chunk);
         integrand_k<FID, R>(x, f, tab);                                  // :188
         bool refine[R];
         unsigned long long m[R];
