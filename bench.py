@@ -302,7 +302,7 @@ def bench_line(args, world, K, B, n_int, elapsed, accepted_total, f_evals, tot, 
                      "ubench_step2_note": "two independent pairs per lane of the per-pair arithmetic "
                                           "(tools/ubench_step2.hip); 76 FP64 + 33 other VALU per pair against the "
                                           "round's 76 + 22 -- a reference figure, not a bound on the kernel",
-                     "kernel": "aq::k_stream<0,false,false,false>", "kernel_avg_us": kern_avg_ms * 1e3,
+                     "kernel": "aq::k_stream<0,false,false,false,12,false>", "kernel_avg_us": kern_avg_ms * 1e3,
                      "flop_per_task": FLOP_PER_TASK, "tasks_per_launch": tasks_per_launch},
         "cpu_baseline": cpu,
         "secondary": secondary,

@@ -88,7 +88,10 @@ constexpr unsigned GSS_DIV = AQ_GSS_DIV;
 #ifndef AQ_HEAP_SEED
 #define AQ_HEAP_SEED 1
 #endif
-// whole-integral jobs (V = 1) seed the top HEAP_D + 1 levels, one node per lane in heap order (k_stream)
+// whole-integral jobs (V = 1) seed the top HEAP_D + 1 levels, one node per lane in heap order: the k_stream
+// instance the batch front end launches (HEAPS, aq_abi.inc batch_heap) -- tiny trees of big batches. The
+// other instances leave the path out: compiled into the bench's instance, unused there, it had cost the
+// bench launch 0.6 % (profiles/r06h: 80.27-80.33 against 79.73-79.91 ms, code placement)
 constexpr bool HEAP_SEED = AQ_HEAP_SEED != 0;
 constexpr int HEAP_D = 4;
 constexpr unsigned HEAP_NODES = (2u << HEAP_D) - 1u;   // 31 nodes + F(A), F(B): 33 lanes
@@ -779,7 +782,7 @@ __device__ unsigned long long g_aq_stamps[MAXG * NW * ST_STRIDE];
 // NWT: waves per workgroup -- NW (12: three per SIMD) for every launch but the unsharded lone ones,
 // which run AQ_LONE_NW (aq_abi.inc launch_stream): a lone integral's set-up and seeding are VALU-bound
 // at three waves per SIMD, and its rounds are bound by one wave's heaviest share.
-template <int FID, bool HIST, bool DIAG, bool PCU, int NWT = NW>
+template <int FID, bool HIST, bool DIAG, bool PCU, int NWT = NW, bool HEAPS = false>
 __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     constexpr int PTT = NWT * 64;   // threads per workgroup
     static_assert(NWT >= 4 && NWT <= NW && NWT % 4 == 0, "whole waves per SIMD, within the LDS rings");
@@ -1231,7 +1234,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 double l2 = A, r2 = B, fl2 = 0.0, fr2 = 0.0, fmid2 = 0.0;
                 // the depth of the seeded pairs' parents (the heap path seeds one level deeper)
                 int Ds = D;
-                if (HEAP_SEED && V == 1u) {
+                if (HEAP_SEED && HEAPS && V == 1u) {
                     // Whole-integral job (V = 1: the wave owns the whole tree, tiny trees of big batches).
                     // Lane q < 31 owns node q of the top five levels in heap order (depth d = log2(q + 1),
                     // k = q + 1 - 2^d), lanes 31 / 32 F(A) / F(B): every node ONCE, where the column path's

@@ -5,7 +5,7 @@ one k_stream instance, finds the innermost loop that holds the round (the loop w
 the v_rcp_f64 of the division), and prints its instruction classes: FP64 VALU, other VALU, SALU,
 LDS, branches. VGPR / SGPR / LDS usage come from the resource-usage remarks.
 
-  python tools/isa_stats.py [--kernel _ZN2aq8k_streamILi0ELb0ELb0ELb0ELi12EEEvNS_12StreamParamsE] [-D...]
+  python tools/isa_stats.py [--kernel _ZN2aq8k_streamILi0ELb0ELb0ELb0ELi12ELb0EEEvNS_12StreamParamsE] [-D...]
   python tools/isa_stats.py --sizes [-D...]     # code bytes of every k_stream instance (device object)
 """
 import argparse
@@ -72,7 +72,7 @@ def classify(ins):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="_ZN2aq8k_streamILi0ELb0ELb0ELb0ELi12EEEvNS_12StreamParamsE")
+    ap.add_argument("--kernel", default="_ZN2aq8k_streamILi0ELb0ELb0ELb0ELi12ELb0EEEvNS_12StreamParamsE")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--mllvm", action="append", default=[], help="an LLVM option (e.g. -amdgpu-sched-strategy=max-ilp)")
     ap.add_argument("--dump", action="store_true", help="print the loop body")
