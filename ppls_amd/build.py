@@ -89,6 +89,8 @@ if __name__ == "__main__":
                 extra.append(a)
             elif a.startswith("--mllvm="):
                 extra += ["-mllvm", a[len("--mllvm="):]]
+            elif a.startswith("-f"):   # code-generation flags (e.g. -falign-loops=64)
+                extra.append(a)
         print("built", build_variant(sys.argv[i + 1], extra))
     else:
         build(force="--force" in sys.argv, verbose=True)
