@@ -724,6 +724,7 @@ __global__ __launch_bounds__(128) void k_reset(Ctl* __restrict__ ctls, int first
 // call. One small launch in place of a reset kernel, a memset and three or four device-to-host
 // copies around every call.
 struct SyncOut {
+    unsigned long long seq;   // the call's sequence number, stored last (the host waits on it)
     SlotSums sums;
     XSum area;
     unsigned long long hist[2 * AQ_MAX_LEVELS];
@@ -731,7 +732,8 @@ struct SyncOut {
 };
 __global__ __launch_bounds__(256) void k_fetch_sync(Ctl* __restrict__ c, unsigned long long* __restrict__ parts,
                                                     const double* __restrict__ parea, int grid, int with_parts,
-                                                    int with_hist, SyncOut* __restrict__ out) {
+                                                    int with_hist, SyncOut* __restrict__ out,
+                                                    unsigned long long seq) {
     const int t = threadIdx.x;
     __shared__ long long sx[XS_LIMBS];
     if (t == 0) out->sums = c->sums;
@@ -751,6 +753,11 @@ __global__ __launch_bounds__(256) void k_fetch_sync(Ctl* __restrict__ c, unsigne
         for (int i = t; i < 2 * AQ_MAX_LEVELS; i += blockDim.x) c->hist[i] = 0ull;
     if (with_parts)
         for (int i = t; i < 2 * grid; i += blockDim.x) parts[i] = 0ull;
+    // the result is complete in host memory: every thread's stores made visible system-wide, then the
+    // sequence number released. The host sees it before the kernel's completion signal would arrive
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // aq_integrate_group: one rank's contribution to the RCCL exchange. sum_row (int64, summed over
