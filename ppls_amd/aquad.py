@@ -275,13 +275,22 @@ class Context:
         return {int(i): int(cu[i]) for i in np.nonzero(cu)[0]}
 
     # -- batch / libm ------------------------------------------------------------------------
-    def integrate_batch(self, a, b, eps, integrand=COSH4):
+    def integrate_batch(self, a, b, eps, integrand=COSH4, out=None):
+        """(area, tasks, accepted) per integral. out: optional (area f64, tasks u64, accepted u64)
+        contiguous arrays of n to write into (a caller that reuses them skips the first-touch page
+        faults of three fresh arrays)."""
         a = np.ascontiguousarray(a, np.float64)
         b = np.ascontiguousarray(b, np.float64)
         n = a.size
-        area = np.empty(n, np.float64)
-        tasks = np.empty(n, np.uint64)
-        acc = np.empty(n, np.uint64)
+        if out is None:
+            area = np.empty(n, np.float64)
+            tasks = np.empty(n, np.uint64)
+            acc = np.empty(n, np.uint64)
+        else:
+            area, tasks, acc = out
+            for x, dt in ((area, np.float64), (tasks, np.uint64), (acc, np.uint64)):
+                if x.dtype != dt or x.shape != (n,) or not x.flags.c_contiguous or not x.flags.writeable:
+                    raise ValueError("out arrays must be writeable contiguous (f64, u64, u64) of the batch's size")
         _check(self.L.aq_integrate_batch(self._h, n, _dp(a), _dp(b), float(eps), integrand, _dp(area), _up(acc),
                                          _up(tasks)), "aq_integrate_batch")
         return area, tasks, acc

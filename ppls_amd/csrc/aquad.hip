@@ -24,10 +24,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -36,6 +43,7 @@
 #include "aq_libm.h"
 #include "aq_device.h"
 #include "aq_stream.h"
+#include "aq_host_pool.h"
 
 #include <rccl/rccl.h>
 
