@@ -260,7 +260,7 @@ def _own_ctx_worker(rank, world, port, q):
 
 def test_gloo_own_context_closed_when_partitions_disagree():
     """a Context integrate_distributed created itself is closed when the partition check
-    raises (it used to leak ~1.3 GiB of device memory per rank on that path)."""
+    raises (it used to leak ~1.2 GiB of device memory per rank on that path)."""
     results = _run(_own_ctx_worker, 2, timeout=120)
     for r in range(2):
         msg, closed = results[r]

@@ -673,7 +673,7 @@ def test_plugin_reference_printout(ctx, trees):
 
 
 def test_context_footprint():
-    """No per-wave area partials or second engine: a fresh context holds ~1.3 GiB -- 262144 result
+    """No per-wave area partials or second engine: a fresh context holds ~1.2 GiB -- 262144 result
     slots (738 MB, r04: 8 x 32768 per launch), the wave cellars (302 MB: 2048 pairs each since r05,
     from 4096), the per-CU count and area words of the first 16384 slots (134 MB; r05: counts of 65536,
     268 MB) and the HBM queue -- of the GPU's
