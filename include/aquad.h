@@ -251,9 +251,10 @@ int aq_cu_task_counters(aq_ctx *ctx, uint64_t *out, int cap, int reset);
  * so a bad bound in a later launch returns AQ_EINVAL after the earlier launches ran: the outputs
  * are then unspecified (not all-or-nothing). Each launch runs its integrals largest-first (a device
  * pre-pass estimates every tree's size; only the order changes, never a result); the host checks,
- * stages and unpacks on up to 8 threads. Environment: AQ_BATCH_SORT=0 keeps the input order,
- * AQ_HOST_THREADS=<n> bounds the host threads, AQ_BATCH_FIRST / AQ_BATCH_LAST set the first / last
- * launch's size (defaults 131072 / no split). */
+ * stages and unpacks on up to 8 threads (a pool the context keeps, created by its first batch call).
+ * Environment: AQ_BATCH_SORT=0 keeps the input order, AQ_HOST_THREADS=<n> bounds the host threads
+ * (read when the pool is created), AQ_BATCH_FIRST / AQ_BATCH_LAST set the first / last launch's size
+ * (defaults 131072 / no split), AQ_BATCH_TRACE=1 prints the call's host phase times on stderr. */
 int aq_integrate_batch(aq_ctx *ctx, size_t n, const double *a, const double *b, double eps, int integrand,
                        double *area, uint64_t *accepted, uint64_t *tasks);
 
