@@ -104,7 +104,12 @@ __global__ __launch_bounds__(256) void k_eval(const double* __restrict__ x, doub
 // correlation 0.9996 (Spearman 0.9995; an offline check with the host integrand). Only the ORDER
 // uses it: the counts and areas of every integral are those of its own tree whatever the order.
 // ------------------------------------------------------------------------------------------------
-constexpr int EST_KEYS = 64;   // size classes: key 0 = largest (descending 6 log2(1 + est))
+// Size classes: key 0 = largest, EST_PER_OCTAVE classes per doubling of 1 + est, so the 256 classes span
+// 2^32 (r06: 64 classes at 6 per octave ran out at est ~ 1 450, ~4 000 tasks -- at eps=1e-10 187 of the
+// 200 golden C3 integrals shared key 0 and the chunk ran unsorted; 8 per octave over 256 classes order
+// them with no pair more than 30 % out of order)
+constexpr int EST_KEYS = 256;
+constexpr double EST_PER_OCTAVE = 8.0;
 // tasks per unit of the estimate: 2.77-2.90 over cosh4 [0,5] at eps = 1e-3 ... 1e-12 and 2.84 for C3's
 // mean at 1e-3 and 1e-10 (an offline check with the host integrand), so a fresh workload's first launch
 // can size its jobs from it (k_batch_scatter)
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(256) void k_batch_estimate(const double2* __restric
                 }
             }
         }
-        const double lg = 6.0 * log2(1.0 + est);
+        const double lg = EST_PER_OCTAVE * log2(1.0 + est);
         const unsigned key = (unsigned)(EST_KEYS - 1) - (unsigned)min((double)(EST_KEYS - 1), lg);
         key_of[i] = key;
         atomicAdd(&s_cnt[key], 1u);
@@ -177,10 +182,11 @@ __global__ __launch_bounds__(256) void k_batch_scatter(const double2* __restrict
                                                        unsigned* __restrict__ perm, unsigned* __restrict__ next,
                                                        const double* __restrict__ est_sum, double* __restrict__ next_est,
                                                        LaunchHint* __restrict__ hint, unsigned max_shares) {
+    static_assert(EST_KEYS == 256, "one class per thread of the block (the scan below)");
     __shared__ unsigned s_off[EST_KEYS], s_cnt[EST_KEYS], s_base[EST_KEYS];
     const unsigned t = threadIdx.x;
     if (blockIdx.x == 0) {
-        if (t < 2u * EST_KEYS) next[t] = 0u;
+        for (unsigned i = t; i < 2u * EST_KEYS; i += blockDim.x) next[i] = 0u;
         if (t == 0) {
             *next_est = 0.0;
             if (hint) {
@@ -190,13 +196,19 @@ __global__ __launch_bounds__(256) void k_batch_scatter(const double2* __restrict
             }
         }
     }
-    if (t < EST_KEYS) {
-        s_cnt[t] = 0u;
-        if (t == 0) {
-            unsigned acc = 0;
-            for (int k = 0; k < EST_KEYS; ++k) { s_off[k] = acc; acc += counts[k]; }
-        }
+    // the classes' offsets: an exclusive scan of the counts, one class per thread (Hillis-Steele in LDS)
+    s_cnt[t] = 0u;
+    s_off[t] = counts[t];
+    __syncthreads();
+    for (unsigned d = 1; d < (unsigned)EST_KEYS; d <<= 1) {
+        const unsigned v = t >= d ? s_off[t - d] : 0u;
+        __syncthreads();
+        s_off[t] += v;
+        __syncthreads();
     }
+    s_base[t] = t ? s_off[t - 1] : 0u;   // inclusive -> exclusive
+    __syncthreads();
+    s_off[t] = s_base[t];
     __syncthreads();
     const int i = (int)(blockIdx.x * blockDim.x + t);
     unsigned key = 0, rank = 0;
