@@ -434,7 +434,16 @@ struct alignas(128) LaunchHint {
     unsigned long long tasks;
     unsigned exits;
     unsigned shares_next;   // 0: no hint yet (the launch uses StreamParams::shares)
+    unsigned long long per_next;   // the tasks per integral shares_next was sized from
 };
+// A launch of few integrals (fewer than the waves) takes more shares per integral than the hint's
+// ~TASKS_PER_JOB jobs would give -- up to one job per wave, with no job below MIN_JOB_TASKS tasks
+// (r06, profiles/r06w: 64 sin(1/x) integrals of 56 k tasks had run as 64 whole-integral jobs on 3072
+// waves, 842 us; 12 / 24 shares each 190 us; at 4096 integrals more shares only cost)
+#ifndef AQ_MIN_JOB_TASKS
+#define AQ_MIN_JOB_TASKS 2048
+#endif
+constexpr unsigned long long MIN_JOB_TASKS = AQ_MIN_JOB_TASKS;
 
 struct StreamParams {
     const double2* bounds;          // [nprob] {a, b} per integral
@@ -470,7 +479,8 @@ struct StreamParams {
     int static_jobs;                // fewer than STATIC_MAXK integrals: static job stride (see k_stream)
     double2 kbounds[PCU_MAXK];      // per-CU launches: the bounds again, as kernel arguments (a scalar load
                                     // with the launch's other arguments, not a cold HBM line at seeding)
-    int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it
+    int adaptive;                   // bit 0: take shares per integral from hint->shares_next; bit 1: update it;
+                                    // bit 2: hint->per_next belongs to it (the HEAPS instance's fill rule)
 };
 
 // Diagnostics record per workgroup (aq_set_diagnostics), accumulated in LDS by every wave:
@@ -873,8 +883,18 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     unsigned shares_main = (unsigned)P.shares;
     int D_main = P.D;
     if (!PCU && (P.adaptive & 1)) {   // (per-CU launches, k < PCU_MAXK, are never adaptive)
-        const unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
+            if (HEAPS && (P.adaptive & 4)) {
+                // (the few-integral / batch instance only, and only when the hint's last writer was this
+                // instance, which also leaves per_next: the bench's instance keeps its code as it was --
+                // its speed moves with code placement)
+                const unsigned long long per =
+                    __hip_atomic_load(&P.hint->per_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned fill = (gridDim.x * (unsigned)NWT + (unsigned)P.nprob - 1u) / (unsigned)P.nprob;
+                const unsigned long long cap = per / MIN_JOB_TASKS;
+                h = uni(max(h, (unsigned)min((unsigned long long)fill, cap)));
+            }
             shares_main = h;
             D_main = seed_depth_job((unsigned long long)h * (unsigned long long)P.nshards);
         }
@@ -2113,6 +2133,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 unsigned long long sh = (per + TASKS_PER_JOB / 2) / TASKS_PER_JOB;
                 sh = sh < 1ull ? 1ull : (sh > (unsigned long long)W ? (unsigned long long)W : sh);
                 __hip_atomic_store(&P.hint->shares_next, (unsigned)sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (HEAPS) __hip_atomic_store(&P.hint->per_next, per, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&P.hint->tasks, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&P.hint->exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }

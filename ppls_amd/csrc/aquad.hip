@@ -193,6 +193,7 @@ __global__ __launch_bounds__(256) void k_batch_scatter(const double2* __restrict
                 const double per = EST_TASKS * *est_sum / (double)max(n, 1);   // predicted tasks per integral
                 const double sh = floor((per + 0.5 * TASKS_PER_JOB) / TASKS_PER_JOB);
                 hint->shares_next = (unsigned)fmin(fmax(sh, 1.0), (double)max_shares);
+                hint->per_next = (unsigned long long)fmax(per, 0.0);
             }
         }
     }
