@@ -885,12 +885,14 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     if (!PCU && (P.adaptive & 1)) {   // (per-CU launches, k < PCU_MAXK, are never adaptive)
         unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
-            if (HEAPS && (P.adaptive & 4)) {
-                // (the few-integral / batch instance only, and only when the hint's last writer was this
-                // instance, which also leaves per_next: the bench's instance keeps its code as it was --
-                // its speed moves with code placement)
+            if constexpr (HEAPS) {
+                // (the few-integral / batch instance only: the bench's instance keeps its code as it was --
+                // its speed moves with code placement). Tasks per integral: per_next when the
+                // hint's last writer was this instance (adaptive bit 2), else from the hint's own shares
+                // when they say more than "one job" (h >= 2: within a factor 1.5)
                 const unsigned long long per =
-                    __hip_atomic_load(&P.hint->per_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    (P.adaptive & 4) ? __hip_atomic_load(&P.hint->per_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : (h >= 2u ? (unsigned long long)h * TASKS_PER_JOB : 0ull);
                 const unsigned fill = (gridDim.x * (unsigned)NWT + (unsigned)P.nprob - 1u) / (unsigned)P.nprob;
                 const unsigned long long cap = per / MIN_JOB_TASKS;
                 h = uni(max(h, (unsigned)min((unsigned long long)fill, cap)));
