@@ -539,6 +539,30 @@ def test_adaptive_job_size_keeps_counts(ctx, oracle, trees):
         ctx.set_level_histograms(True)
 
 
+@pytest.mark.parametrize("k", [16, 64, 700])
+def test_few_integrals_fill_the_waves(ctx, trees, k):
+    """Launches of fewer integrals than the GPU's waves (16 .. W - 1, unsharded) run the few-integral /
+    batch instance, which raises the job-size hint's shares per integral to fill the waves (up to one
+    job per wave, none below 2 k tasks; DESIGN §2.1 *Few integrals*). Its first launch (no hint), its
+    hinted launches, and a switch to and from a launch of more integrals than waves (the bench's
+    instance, which leaves no per-integral task count in the hint) keep every count exact and every
+    area within the tolerance of the golden tree's quad sum -- for the skewed sin(1/x) tree and cosh4."""
+    from ppls_amd import SIN_RECIP
+    big = ctx.num_workers + 64
+    ctx.set_level_histograms(False)
+    try:
+        for name, integrand, a0, b0, eps in (("sin_recip_eps1e-9", SIN_RECIP, 1e-4, 1.0, 1e-9),
+                                             ("cosh4_eps1e-8", 0, 0.0, 5.0, 1e-8)):
+            g = trees[name]
+            for n in (k, k, big, k):
+                ctx.integrate_many_async(np.full(n, a0), np.full(n, b0), eps, first_slot=0, integrand=integrand)
+                rs = [ctx.fetch(i) for i in (0, n // 2, n - 1)]
+                assert all((r.tasks, r.accepted) == (g["tasks"], g["leaves"]) for r in rs), (name, n)
+                assert all(_area_ok(r.area, g["area_quad"]) for r in rs), (name, n)
+    finally:
+        ctx.set_level_histograms(True)
+
+
 # Deep trees (up to 150 M tasks, depth 31, in one launch), pinned by the reference binary's own task
 # totals (tests/golden/deep.json, make_golden.py deep): alone and as a small batch.
 @pytest.mark.parametrize("name", ["cosh4_eps1e-14", "cosh4_eps1e-15", "cosh4_eps1e-16"])
