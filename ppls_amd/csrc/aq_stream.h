@@ -208,7 +208,8 @@ constexpr unsigned SHARE_ROT = 1021;   // static-job launches: share offset from
 // left beside the pair block holds 12)
 constexpr int PCU_MAXK = 12;
 constexpr int PCU_ROW = PCU_MAXK - 1;   // per-CU LDS rows: tags < k < PCU_MAXK
-constexpr int STATIC_MAXK = 16;     // launches of fewer integrals (unsharded): one share per wave, static stride
+constexpr int STATIC_MAXK = 16;     // sharded launches of fewer integrals: one share per wave, static stride
+                                    // (unsharded: below PCU_MAXK, aq_abi.inc launch_stream)
 // The pair word dt: bits 0-7 the pair's depth (the depth of its two tasks), bits 8-30 the integral
 // (tag), bit 31 SPAN_BIT. SPAN_BIT (cosh4): the pair's interval lies where glibc's cosh takes its exp
 // path (cosh_main_span) -- set at seeding, inherited by the children (sub-intervals), so a round tests

@@ -272,9 +272,9 @@ def test_many_integrals_one_launch(ctx, oracle, trees):
 
 @pytest.mark.parametrize("k", [2, 11, 12, 15, 16])
 def test_few_integrals_static_jobs(ctx, oracle, trees, k):
-    """Launches of fewer than 16 integrals seed one share per wave with a static, rotated stride
-    (per-CU instance below 12 integrals, the bulk instance from 12 to 15); 16 claims jobs. Every
-    integral is its own exact tree; the cosh4 [0,5] ones match the golden counts."""
+    """Launches of fewer than 12 integrals (the per-CU instance) seed one share per wave with a static,
+    rotated stride; from 12 on (r06: from 16) they claim jobs filled to one per wave. Every integral is
+    its own exact tree; the cosh4 [0,5] ones match the golden counts."""
     g = trees["cosh4_eps1e-8"]
     a, b = oracle.batch_bounds(k)
     a[0], b[0] = 0.0, 5.0
