@@ -161,6 +161,9 @@ __device__ __forceinline__ double expm1_glibc_small(double x) {
 #ifndef AQ_RCP_NEWTON
 #define AQ_RCP_NEWTON 2
 #endif
+#ifndef AQ_SIN_RECIP_RN
+#define AQ_SIN_RECIP_RN 1   // sin(1/x): recip_rn in place of the compiler's division (bit-identical)
+#endif
 template <int NEWTON = AQ_RCP_NEWTON>
 __device__ __forceinline__ double half_recip_n(double t) {
     double y = __builtin_amdgcn_rcp(t);
@@ -179,6 +182,22 @@ __device__ __forceinline__ double half_recip_n(double t) {
     return __fma_rn(r, y, q);
 }
 __device__ __forceinline__ double half_recip(double t) { return half_recip_n<>(t); }
+// 1.0 / x, correctly rounded, for the config-4 integrand's sin(1.0/(arg)): the same sequence with
+// numerator 1 -- the compiler's IEEE division minus its scale / fmas scaling / fixup steps, identities
+// while x and 1/x are normal (every nonzero bound is at least 2^-900 and at most 2^900 in magnitude,
+// aq_abi.inc bounds_ok; x = 0, a midpoint of a symmetric interval, gives NaN either way). r06: 4 VALU
+// fewer per evaluation, sin(1/x) launch times within noise (profiles/r06zj); tests/test_gpu.py
+// test_device_sin_recip_bit_exact pins it to host libm.
+__device__ __forceinline__ double recip_rn(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double e = __fma_rn(-x, y, 1.0);
+        y = __fma_rn(y, e, y);
+    }
+    const double r = __fma_rn(-x, y, 1.0);
+    return __fma_rn(r, y, y);
+}
 
 // glibc's `half*t + half/t` is RN(RN(0.5*t) + h) with h = RN(0.5/t); 0.5*t is exact for the
 // normal t of this range, so RN(0.5*t + h) -- one fma(t, 0.5, h) -- is the same value, bit for bit,
@@ -319,7 +338,7 @@ __device__ __forceinline__ double integrand(double x, const ExpEntry* __restrict
     } else if constexpr (FID == F_USER) {
         return user::F(x, tab);
     } else {
-        return sin_glibc(1.0 / x, sin_table(tab));   // config 4: sin(1.0/(arg)); tab: stage_f_table
+        return sin_glibc(AQ_SIN_RECIP_RN ? recip_rn(x) : 1.0 / x, sin_table(tab));   // config 4: sin(1.0/(arg))
     }
 }
 
@@ -468,7 +487,7 @@ __device__ __forceinline__ void integrand_k(const double (&x)[K], double (&f)[K]
         for (int k = 0; k < K; ++k) f[k] = user::F(x[k], tab);
     } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) f[k] = sin_glibc(1.0 / x[k], sin_table(tab));
+        for (int k = 0; k < K; ++k) f[k] = sin_glibc(AQ_SIN_RECIP_RN ? recip_rn(x[k]) : 1.0 / x[k], sin_table(tab));
     }
 }
 
