@@ -166,7 +166,8 @@ int aq_integrate_many_async(aq_ctx *ctx, int integrand, int k, const double *a, 
                             int max_depth, int shard, int nshards, int first_slot);
 /* Like aq_integrate_many_async with a per-integral shard: integral i is shard shard[i] of nshards
  * (the partition of aq_integrate_shard; every launch of one nshards uses the same partition, so any
- * rank may run any shard of any integral -- the rebalanced multi-GPU batch, ppls_amd/dist.py). */
+ * rank may run any shard of any integral -- the rebalanced multi-GPU batch, ppls_amd/dist.py).
+ * nshards == 1 (every shard[i] 0: whole integrals) is an unsharded launch, as aq_integrate_many_async. */
 int aq_integrate_mixed_async(aq_ctx *ctx, int integrand, int k, const double *a, const double *b,
                              const int32_t *shard, int nshards, double eps, int max_depth, int first_slot);
 int aq_fetch(aq_ctx *ctx, int slot, aq_result *res);
