@@ -563,6 +563,40 @@ def test_few_integrals_fill_the_waves(ctx, trees, k):
         ctx.set_level_histograms(True)
 
 
+def test_random_batches_match_oracle_across_launch_shapes(ctx, oracle):
+    """The r06 launch shapes against the CPU restatement on random bounds at tolerances no golden
+    fixture holds: a one-chunk sorted batch (size classes, the pre-pass stream, the host pool, the
+    batch instance's fill rule) at eps=1e-6, few-integral launches (static per-CU deal, claimed filled
+    jobs; first and hinted) of cosh4 at 1e-7 and of sin(1/x) at 1e-8. Counts exact, areas within the
+    per-tree tolerance of the oracle's."""
+    from ppls_amd import SIN_RECIP
+    a, b = oracle.batch_bounds(3000)
+    area, tasks, acc = ctx.integrate_batch(a, b, 1e-6)
+    oa, ot, ol = oracle.integrate_batch(a, b, 1e-6)
+    assert (tasks == ot).all() and (acc == ol).all()
+    assert np.all(np.abs(area - oa) <= AREA_RTOL * np.abs(oa))
+    ctx.set_level_histograms(False)
+    try:
+        for k in (5, 14, 40):
+            ak, bk = a[:k], b[:k]
+            oa, ot, ol = oracle.integrate_batch(ak, bk, 1e-7)
+            for _ in range(2):   # the first launch of the workload, then a hinted one
+                ctx.integrate_many_async(ak, bk, 1e-7, first_slot=0)
+                rs = [ctx.fetch(i) for i in range(k)]
+                assert [(r.tasks, r.accepted) for r in rs] == [(int(t), int(l)) for t, l in zip(ot, ol)], k
+                assert all(abs(r.area - w) <= AREA_RTOL * abs(w) for r, w in zip(rs, oa)), k
+        k = 24
+        sa, sb = 1e-4 + a[:k] / 5.0, 1e-4 + b[:k] / 5.0 + 1e-3
+        oa, ot, ol = oracle.integrate_batch(sa, sb, 1e-8, integrand=oracle.SIN_RECIP)
+        for _ in range(2):
+            ctx.integrate_many_async(sa, sb, 1e-8, first_slot=0, integrand=SIN_RECIP)
+            rs = [ctx.fetch(i) for i in range(k)]
+            assert [(r.tasks, r.accepted) for r in rs] == [(int(t), int(l)) for t, l in zip(ot, ol)]
+            assert all(abs(r.area - w) <= AREA_RTOL * abs(w) for r, w in zip(rs, oa))
+    finally:
+        ctx.set_level_histograms(True)
+
+
 # Deep trees (up to 150 M tasks, depth 31, in one launch), pinned by the reference binary's own task
 # totals (tests/golden/deep.json, make_golden.py deep): alone and as a small batch.
 @pytest.mark.parametrize("name", ["cosh4_eps1e-14", "cosh4_eps1e-15", "cosh4_eps1e-16"])
