@@ -37,7 +37,8 @@ def main():
     a, b = splitmix64_bounds(max(256, args.c3))
     ctx.integrate_many_async(a[:256], b[:256], 1e-3)
     out["batch256_ok"] = [ctx.fetch(i).accepted for i in range(256)] == batch["leaves_eps1e-3_first256"]
-    tag = {1e-10: "cosh4_eps1e-10", 1e-12: "cosh4_eps1e-12", 1e-8: "cosh4_eps1e-8"}[args.eps]
+    tag = {1e-10: "cosh4_eps1e-10", 1e-12: "cosh4_eps1e-12", 1e-8: "cosh4_eps1e-8", 1e-6: "cosh4_eps1e-6",
+           1e-3: "cosh4_eps1e-3"}[args.eps]
     g = trees[tag]
     k = args.k
     ctx.integrate_many_async(np.zeros(k), np.full(k, 5.0), args.eps)
