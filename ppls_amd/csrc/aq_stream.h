@@ -883,6 +883,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     // shares per integral: the host's choice, or the job-size hint the previous adaptive launch left
     unsigned shares_main = (unsigned)P.shares;
     int D_main = P.D;
+    unsigned long long per_hint = 0;   // HEAPS: the hint's tasks per integral (0: unknown)
     if (!PCU && (P.adaptive & 1)) {   // (per-CU launches, k < PCU_MAXK, are never adaptive)
         unsigned h = uni(__hip_atomic_load(&P.hint->shares_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (h) {
@@ -897,6 +898,7 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
                 const unsigned fill = (gridDim.x * (unsigned)NWT + (unsigned)P.nprob - 1u) / (unsigned)P.nprob;
                 const unsigned long long cap = per / MIN_JOB_TASKS;
                 h = uni(max(h, (unsigned)min((unsigned long long)fill, cap)));
+                per_hint = per;
             }
             shares_main = h;
             D_main = seed_depth_job((unsigned long long)h * (unsigned long long)P.nshards);
@@ -939,16 +941,25 @@ __global__ __launch_bounds__(NWT * 64) void k_stream(StreamParams P) {
     // lie spread over the whole interval instead of side by side, so no workgroup holds only the
     // costly end of it
     const bool static_jobs = PCU || P.static_jobs != 0;
-    unsigned job = static_jobs ? wid * gridDim.x + bid : w_all;
+    // (HEAPS, the batch instance: its launches run size-ordered chunks, whose first W jobs would give
+    // workgroup 0 the 12 largest trees and the last workgroup the 12 smallest of them -- dealt transposed,
+    // every CU gets one job of each size band; r06)
+    unsigned job = (static_jobs || HEAPS) ? wid * gridDim.x + bid : w_all;
     bool job_pending = false;     // `job` is still in flight in lane 0's `claim`
     unsigned claim = 0;           // lane 0: the prefetched claim (jobs W + claim .. + jpc - 1)
     // jobs per claim. Whole-integral jobs of a big batch are short (C3 at eps=1e-3: ~1 400 tasks), and
     // one claim each made the job counter a serial fan-in (65536 claims on one line, ~10 ns each: a
     // static deal of the same launch ran 815 -> 543 us). Such launches claim a run of consecutive
     // jobs at once -- at least 4 claims per wave stay, for the balance -- one job otherwise.
-    const unsigned jpc = (!static_jobs && shares_main == 1u && P.nshards == 1 && JOB_RUN_MAX > 1)
-                             ? max(1u, min((unsigned)JOB_RUN_MAX, total_jobs / (4u * W)))
-                             : 1u;
+    // (HEAPS: a run holds at most ~TASKS_PER_JOB tasks by the hint's tasks per integral -- in a size-
+    // ordered chunk consecutive jobs are alike, and runs of 10 of its largest 66 k-task trees had made a
+    // 262144-integral eps=1e-8 batch launch 8 % slower than the same integrals unsorted, r06)
+    unsigned jpc = (!static_jobs && shares_main == 1u && P.nshards == 1 && JOB_RUN_MAX > 1)
+                       ? max(1u, min((unsigned)JOB_RUN_MAX, total_jobs / (4u * W)))
+                       : 1u;
+    if constexpr (HEAPS) {
+        if (per_hint) jpc = uni(max(1u, min(jpc, (unsigned)min((unsigned long long)TASKS_PER_JOB / per_hint, 64ull))));
+    }
     unsigned job_end = job + 1u;  // end of the claimed run `job` belongs to
     unsigned claim_n = jpc;       // jobs the claim in flight takes (guided: shrinks near the end)
     unsigned err = 0;
