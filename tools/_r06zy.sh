@@ -1,0 +1,17 @@
+#!/bin/bash
+# r06zy: the transposed first deal in every instance (libaquad_dealt) against the batch instance only
+# (libaquad) -- the bench launch + lone (3 alternating passes), and size-sorted vs random cosh4 launches
+set -u
+OUT=gpurun_out/r06zy; mkdir -p $OUT
+ROUNDS=3 K=32768 REPS=2 SINGLE=20 C3=0 AB_GLOB="libaquad*.so" bash tools/ab.sh r06zy > $OUT/ab.txt 2>&1 || { tail -5 $OUT/ab.txt; exit 1; }
+grep -h "" $OUT/ab.txt | tail -3
+python3 - <<'PY'
+import json,glob,collections
+res=collections.defaultdict(list)
+for f in sorted(glob.glob('gpurun_out/ab_r06zy/libaquad*.[0-9].json')):
+    n=f.split('/')[-1].rsplit('.',2)[0]
+    try: res[n].append(json.load(open(f)))
+    except Exception: pass
+for n,v in res.items():
+    print(n, 'bench_launch_us', [round(x['kernel_us']) for x in v if 'kernel_us' in x], 'lone_us', [round(x['single_us'],2) for x in v if 'single_us' in x])
+PY
